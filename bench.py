@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X-native Chorin projection step (BASELINE.json metric:
+"MLUPS + achieved HBM GB/s, 512^3 projection step, 1/2/4/8xMI355X").
+
+Workload (BASELINE.json configs[2]): 512^3 lid-driven
+cavity, Re = 1000 (nu = 1e-3), dt = 1e-4, projection_hip with the CPU
+reference's CG settings (rel 1e-6, abs 1e-10). Fields are synthetic (the
+cavity starts at rest), generated and kept resident in HBM; a "step" is one
+full projection step (predictor, CG pressure solve to convergence,
+corrector). value = interior cells updated per second over all ranks, in
+MLUPS.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+For N > 1 launch with torch.distributed.run (one rank per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Algorithmic HBM bytes per interior cell:
+BYTES_SWEEP_A = 40.0    # read r, p_old, x; write p_new, x
+BYTES_SWEEP_B = 24.0    # read p, r; write r
+BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
+BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=512, help="points per axis")
+    ap.add_argument("--re", type=float, default=1000.0)
+    ap.add_argument("--dt", type=float, default=1e-4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cg-iters", type=int, default=10,
+                    help="CG iterations timed in the CPU baseline sample")
+    ap.add_argument("--kchunk", type=int, default=0)
+    return ap.parse_args()
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_env()
+    import torch  # noqa: F401  (imported first: one HIP runtime in the process)
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    from cfd_amd import _abi as A
+    from cfd_amd import _native, api
+
+    lib = _native.hip()
+    if lib.hip_projection_available() != 1:
+        raise SystemExit("bench: no HIP device")
+    if world > 1:
+        raise SystemExit("bench: multi-GPU Z-slab path not built yet")
+
+    n = args.n
+    nu = 1.0 / args.re
+    g = api.Grid(n, n, n, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
+    params = api.validation_params(args.dt, nu)
+    ctx = api.HipProjection(n, n, n, device=local, kchunk=args.kchunk)
+    for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
+        ctx.fill(fid, 0.0)
+    ctx.set_density(1.0)
+    # caller BCs (lid_driven_cavity_common.h:142-148, 3-D form): u = 1 on the lid
+    ctx.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
+    ctx.apply_dirichlet(A.HIP_FIELD_V, api.dirichlet())
+    ctx.apply_dirichlet(A.HIP_FIELD_W, api.dirichlet())
+    ctx.apply_scalar_bc(A.HIP_FIELD_P, A.BC_TYPE_NEUMANN)
+    ctx.synchronize()
+
+    def step():
+        s = ctx.step_device(g, params)
+        if s != A.CFD_SUCCESS:
+            raise RuntimeError(f"step failed {s}: {_native.last_error()}")
+        return ctx.poisson_stats().iterations
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = [step() for _ in range(args.steps)]
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ctx.enable_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+
+    n_int = (n - 2) ** 3
+    ms_step = elapsed / args.steps * 1e3
+    mlups = n_int * args.steps * world / elapsed / 1e6
+    k_mean = sum(iters) / len(iters)
+    step_bytes = (BYTES_STEP_FIXED_SURVEY + BYTES_CG_ITER_SURVEY * k_mean) * n_int
+    gbps_step = step_bytes * args.steps * world / elapsed / 1e9
+
+    kt = ctx.timing()
+    ms_a, n_a = kt["cg_sweep_a"]
+    ms_b, n_b = kt["cg_sweep_b"]
+    avg_a = ms_a / max(n_a, 1)
+    avg_b = ms_b / max(n_b, 1)
+    ach_a = BYTES_SWEEP_A * n_int / (avg_a * 1e-3) / 1e9 if n_a else None
+    ach_b = BYTES_SWEEP_B * n_int / (avg_b * 1e-3) / 1e9 if n_b else None
+    cg_iter_ms = avg_a + avg_b
+    cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_int / (cg_iter_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n, args, k_mean)
+
+    if rank == 0:
+        out = {
+            "metric": "MLUPS + achieved HBM GB/s, 512^3 projection step, 1/2/4/8xMI355X",
+            "value": round(mlups, 3),
+            "unit": "MLUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (cavity at rest + lid BC, generated in HBM)",
+            "config": {"workload": f"{n}^3 lid-driven cavity Re={args.re:g}, dt={args.dt:g}, "
+                                   "projection_hip (CG rel 1e-6)",
+                       "grid": [n, n, n], "interior_cells": n_int,
+                       "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
+            "achieved_GBps": round(gbps_step, 1),
+            "cg_iters_per_step": iters,
+            "cg_iter_ms": round(cg_iter_ms, 4),
+            "cg_iter_GBps_survey80": round(cg_iter_gbps_survey, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_cg_sweep_a",
+                         "achieved": round(ach_a, 1) if ach_a else None,
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach_a / HBM_PEAK_GBPS, 4) if ach_a else None,
+                         "traffic": None, "bytes_per_cell": BYTES_SWEEP_A,
+                         "avg_launch_ms": round(avg_a, 4)},
+            "kernels": {k: {"total_ms": round(v[0], 3), "launches": v[1],
+                            "avg_ms": round(v[0] / v[1], 4) if v[1] else None}
+                        for k, v in kt.items() if v[1]},
+            "sweep_b": {"achieved": round(ach_b, 1) if ach_b else None,
+                        "bytes_per_cell": BYTES_SWEEP_B},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(n, args, k_gpu):
+    """The oracle (OpenMP port of the reference projection) timed on this host
+    on a bounded sample of the same step: predictor, divergence and corrector in
+    full and `cpu_cg_iters` CG iterations on the same 512^3 cavity state; the
+    step time is those phases + k_gpu x the measured CG iteration time."""
+    import numpy as np
+
+    from cfd_amd import _abi as A
+    from cfd_amd import api
+    from oracle import oracle
+
+    try:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    except Exception:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, 64))
+    oracle.set_threads(threads)
+    g = api.Grid(n, n, n, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
+    f = api.FlowField(n, n, n)
+    f.rho[...] = 1.0
+    api.cavity_bc(f, 1.0)
+    p = api.validation_params(args.dt, 1.0 / args.re)
+    oracle.lib().oracle_set_poisson_cap(args.cpu_cg_iters)
+    t0 = time.perf_counter()
+    s, _, it = oracle.projection_step(f, g, p)
+    wall = time.perf_counter() - t0
+    oracle.lib().oracle_set_poisson_cap(0)
+    ph = oracle.last_phase_ms()
+    t_cg_iter = ph[2] / max(it, 1) / 1e3
+    t_step = (ph[0] + ph[1] + ph[3]) / 1e3 + k_gpu * t_cg_iter
+    n_int = (n - 2) ** 3
+    return {"value": round(n_int / t_step / 1e6, 4), "unit": "MLUPS", "cores": threads,
+            "kind": "port",
+            "sample": (f"{n}^3 cavity step 1 on the host: predictor+divergence+corrector timed "
+                       f"in full, {it} CG iterations timed ({t_cg_iter*1e3:.1f} ms/iter) and "
+                       f"scaled to the GPU's {k_gpu:.0f} iterations/step; OpenMP x{threads}; "
+                       f"sample wall {wall:.1f} s"),
+            "cg_iter_ms": round(t_cg_iter * 1e3, 2), "status": s}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,719 @@
+// kernels.hpp -- gfx950 device code for the Chorin projection step.
+//
+// Layout in HBM: every field is an SoA fp64 array with a padded row pitch
+// `px` (multiple of 8 doubles = 64 B) and plane pitch `ps` = px*ny, x fastest.
+// The reference layout idx = k*nx*ny + j*nx + i (lib/include/cfd/core/indexing.h)
+// is recovered with px = nx; uploads/downloads convert with 2-D copies.
+//
+// Stencil sweeps use 2.5-D tiles: a 256-thread workgroup owns a 64 (x) by 4 (y)
+// column tile and marches a chunk of `kc` planes in z, keeping the k-1/k/k+1
+// values of its own column in registers so each plane is read once from HBM;
+// x/y neighbours come from the L1/L2 lines the neighbouring lanes and waves
+// of the same tile just loaded. One wavefront = one 64-wide x row, so every
+// load is a fully coalesced 512-B row segment.
+//
+// Reductions are deterministic: per-thread sums in a fixed k order, a fixed
+// 64-lane shuffle tree, a fixed cross-wave order, one partial per workgroup,
+// and the last-arriving workgroup (agent-scope ticket) sums the partials in
+// index order. The partial hand-off follows the sc1 write-through protocol
+// (MI355X_MICROARCH.md "Valid forms", first table row): one lane stores the
+// partial with an agent-scope relaxed store, waits vmcnt(0), then takes the
+// ticket; the last workgroup reads every partial with agent-scope loads.
+//
+// All arithmetic is written in the reference's operation order and the file
+// is compiled with -ffp-contract=off, so every per-cell value is bitwise the
+// reference's; only the summation order of the CG dot products differs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfdhip {
+
+constexpr int TX = 64;       // x extent of a tile = one wavefront
+constexpr int TY = 4;        // y rows per tile
+constexpr int NT = TX * TY;  // threads per workgroup
+constexpr int NWAVE = NT / 64;
+
+// Poisson status codes (poisson_solver.h:83-89)
+constexpr int ST_CONVERGED = 0;
+constexpr int ST_MAX_ITER = 1;
+constexpr int ST_STAGNATED = 3;
+
+struct Geo {
+    int nx, ny, nz;        // points of the local array, boundary included
+    long long px;          // row pitch (doubles)
+    long long ps;          // plane pitch (doubles)
+    long long sz;          // z stencil offset: ps in 3-D, 0 in 2-D (reference stride_z)
+    int k0, k1;            // interior planes [k0, k1)
+    int kc;                // planes per tile
+    int tiles_x, tiles_y, tiles_z;
+};
+
+struct Lap {
+    double dx2_inv, dy2_inv, inv_dz2;  // linear_solver_cg.c:103-110
+};
+
+// Device-resident CG state; written only by the finishing (last) workgroup.
+struct CgState {
+    double rho;     // (r, r) of the current residual
+    double alpha;   // alpha of the most recent sweep A
+    double beta;    // beta for the next sweep A
+    double pAp;
+    double res;     // current residual 2-norm
+    double res0;    // initial residual
+    double tol;     // max(rel_tol * res0, abs_tol)
+    double abs_tol;
+    int iterations; // completed iterations (reference stats->iterations)
+    int done;       // no further iteration may run
+    int status;     // poisson_solver_status_t
+    int pending;    // x still lacks alpha * p of the last iteration
+    int max_iter;
+    int check_interval;
+    int pad0, pad1;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+    unsigned long long b =
+        __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __longlong_as_double((long long)b);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off, 64));
+    return v;
+}
+
+// Sum over the workgroup; result valid in thread 0. `sh` holds NWAVE doubles.
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) s += sh[w];
+    }
+    __syncthreads();
+    return s;
+}
+
+// Grid-wide deterministic sum. Returns true (in every thread) for the
+// last-arriving workgroup; its thread 0 then holds the grid total.
+__device__ __forceinline__ bool grid_sum_last(double block_total, double* partials,
+                                              unsigned* counter, double* sh, int* flag,
+                                              double& total) {
+    if (threadIdx.x == 0) {
+        store_sc1(&partials[blockIdx.x], block_total);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        *flag = (t == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (*flag == 0) return false;
+    double s = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += NT) s += load_sc1(&partials[b]);
+    total = block_sum(s, sh);
+    if (threadIdx.x == 0)
+        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// Order-preserving encoding of doubles into uint64 for atomicMax.
+__device__ __forceinline__ unsigned long long ord_enc(double d) {
+    unsigned long long b = (unsigned long long)__double_as_longlong(d);
+    return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+}
+
+struct TileCoord {
+    int i, j, kb, ke;
+    bool active;
+};
+
+__device__ __forceinline__ TileCoord tile_coord(const Geo& g, int t) {
+    TileCoord c;
+    const int tx = t % g.tiles_x;
+    const int rest = t / g.tiles_x;
+    const int ty = rest % g.tiles_y;
+    const int tz = rest / g.tiles_y;
+    c.i = tx * TX + (threadIdx.x & 63);
+    c.j = ty * TY + (threadIdx.x >> 6);
+    c.kb = g.k0 + tz * g.kc;
+    c.ke = min(c.kb + g.kc, g.k1);
+    c.active = (c.i >= 1) && (c.i <= g.nx - 2) && (c.j >= 1) && (c.j <= g.ny - 2);
+    return c;
+}
+
+__device__ __forceinline__ long long cidx(const Geo& g, int i, int j, int k) {
+    return (long long)k * g.ps + (long long)j * g.px + i;
+}
+
+// Laplacian exactly as linear_solver_cg.c:113-116 groups it.
+__device__ __forceinline__ double lap7(const Lap& L, double c, double xm, double xp, double ym,
+                                       double yp, double zm, double zp) {
+    return ((xp - (2.0 * c) + xm) * L.dx2_inv) + ((yp - (2.0 * c) + ym) * L.dy2_inv) +
+           ((zp + zm - (2.0 * c)) * L.inv_dz2);
+}
+
+// ---------------------------------------------------------------------------
+// CG setup: r = -rhs + lap(x) (linear_solver_cg.c:134-158) and rho = (r, r).
+// FROM_VEL: rhs = (rho/dt) * div(u*) computed on the fly exactly as
+// solver_projection.c:195-214 (the rhs array is never materialised for CG);
+// otherwise rhs is read from memory. WRITE_RHS stores the rhs for the
+// relaxation solvers, which re-read it every sweep.
+// ---------------------------------------------------------------------------
+struct DivCoef {
+    double two_dx, two_dy;   // 2.0*dx, 2.0*dy (divided by, as the reference does)
+    double inv_2dz;          // 1/(2dz), 0 in 2-D
+    double rho_over_dt;
+};
+
+template <bool FROM_VEL, bool WRITE_RHS, bool WITH_RR>
+__global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
+                                                 const double* __restrict__ us,
+                                                 const double* __restrict__ vs,
+                                                 const double* __restrict__ ws,
+                                                 double* __restrict__ rhs,
+                                                 const double* __restrict__ x,
+                                                 double* __restrict__ r, CgState* st,
+                                                 double* partials, unsigned* counter,
+                                                 double rel_tol, double abs_tol, int max_iter,
+                                                 int check_interval) {
+    __shared__ double sh[NWAVE];
+    __shared__ int flag;
+    double acc = 0.0;
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        double xm = x[idx - g.sz], xc = x[idx];
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            double xp = x[idx + g.sz];
+            double b;
+            if (FROM_VEL) {
+                double dus = (us[idx + 1] - us[idx - 1]) / dc.two_dx;
+                double dvs = (vs[idx + g.px] - vs[idx - g.px]) / dc.two_dy;
+                double dws = (ws[idx + g.sz] - ws[idx - g.sz]) * dc.inv_2dz;
+                double div = dus + dvs + dws;
+                b = dc.rho_over_dt * div;
+                if (WRITE_RHS) rhs[idx] = b;
+            } else {
+                b = rhs[idx];
+            }
+            double lap = lap7(L, xc, x[idx - 1], x[idx + 1], x[idx - g.px], x[idx + g.px], xm, xp);
+            double rv = -b + lap;
+            if (WITH_RR) {
+                r[idx] = rv;
+                acc += rv * rv;
+            }
+            xm = xc;
+            xc = xp;
+        }
+    }
+    if (!WITH_RR) return;
+    double bt = block_sum(acc, sh);
+    double tot;
+    if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
+        double res0 = sqrt(tot);                   // linear_solver_cg.c:345
+        double tol = rel_tol * res0;               // :352-355
+        if (tol < abs_tol) tol = abs_tol;
+        st->rho = tot;
+        st->res0 = res0;
+        st->res = res0;
+        st->tol = tol;
+        st->abs_tol = abs_tol;
+        st->alpha = 0.0;
+        st->beta = 0.0;
+        st->pAp = 0.0;
+        st->iterations = 0;
+        st->pending = 0;
+        st->max_iter = max_iter;
+        st->check_interval = check_interval;
+        if (res0 < abs_tol || max_iter <= 0) {     // :357-365
+            st->done = 1;
+            st->status = (res0 < abs_tol) ? ST_CONVERGED : ST_MAX_ITER;
+        } else {
+            st->done = 0;
+            st->status = ST_MAX_ITER;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CG sweep A of iteration `it`:
+//   p_it = r_it + beta p_{it-1}          (p_0 = r_0), written to pnew
+//   (p_it, A p_it) with A = -lap, A p computed in registers, never stored
+//   x += alpha_{it-1} p_{it-1}           (the x update of the previous
+//                                         iteration, deferred into this sweep)
+// HBM per interior cell: read r, pold, x; write pnew, x (FIRST: read r, write pnew).
+// ---------------------------------------------------------------------------
+template <bool FIRST>
+__global__ __launch_bounds__(NT) void k_cg_sweep_a(Geo g, Lap L, const double* __restrict__ r,
+                                                   const double* __restrict__ pold,
+                                                   double* __restrict__ pnew,
+                                                   double* __restrict__ x, CgState* st,
+                                                   double* partials, unsigned* counter, int it) {
+    __shared__ double sh[NWAVE];
+    __shared__ int flag;
+    if (st->done) return;
+    const double beta = FIRST ? 0.0 : st->beta;
+    const double alpha_prev = FIRST ? 0.0 : st->alpha;
+    double acc = 0.0;
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+#define PDIR(ix) (FIRST ? r[ix] : (r[ix] + beta * pold[ix]))
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        double pm = PDIR(idx - g.sz);
+        double pc = PDIR(idx);
+        double poc = FIRST ? 0.0 : pold[idx];
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            const long long ip = idx + g.sz;
+            double pop = FIRST ? 0.0 : pold[ip];
+            double pp = FIRST ? r[ip] : (r[ip] + beta * pop);
+            double lap = lap7(L, pc, PDIR(idx - 1), PDIR(idx + 1), PDIR(idx - g.px),
+                              PDIR(idx + g.px), pm, pp);
+            double Ap = -lap;
+            acc += pc * Ap;
+            pnew[idx] = pc;
+            if (!FIRST) x[idx] += alpha_prev * poc;
+            pm = pc;
+            pc = pp;
+            poc = pop;
+        }
+#undef PDIR
+    }
+    double bt = block_sum(acc, sh);
+    double tot;
+    if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
+        st->pAp = tot;
+        if (fabs(tot) < 1e-30) {                    // CG_CHECK_BREAKDOWN(p_dot_Ap)
+            st->done = 1;
+            st->status = ST_STAGNATED;
+            st->iterations = it + 1;
+            st->pending = 0;
+        } else {
+            st->alpha = st->rho / tot;
+            st->pending = 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CG sweep B of iteration `it`: r -= alpha A p (A p recomputed from pnew,
+// bitwise equal to sweep A's), rho_new = (r, r), convergence and beta.
+// HBM per interior cell: read p, r; write r.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_cg_sweep_b(Geo g, Lap L, const double* __restrict__ p,
+                                                   double* __restrict__ r, CgState* st,
+                                                   double* partials, unsigned* counter, int it) {
+    __shared__ double sh[NWAVE];
+    __shared__ int flag;
+    if (st->done) return;
+    const double malpha = -st->alpha;
+    double acc = 0.0;
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        double pm = p[idx - g.sz];
+        double pc = p[idx];
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            double pp = p[idx + g.sz];
+            double lap = lap7(L, pc, p[idx - 1], p[idx + 1], p[idx - g.px], p[idx + g.px], pm, pp);
+            double Ap = -lap;
+            double rn = r[idx] + malpha * Ap;       // axpy(-alpha, Ap, r)
+            r[idx] = rn;
+            acc += rn * rn;
+            pm = pc;
+            pc = pp;
+        }
+    }
+    double bt = block_sum(acc, sh);
+    double tot;
+    if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
+        // linear_solver_cg.c:391-438
+        double res = sqrt(tot);
+        st->res = res;
+        st->iterations = it + 1;
+        const bool check = (it % st->check_interval) == 0;
+        const bool conv = (res < st->tol) || (res < st->abs_tol);
+        if (check && conv) {
+            st->done = 1;
+            st->status = ST_CONVERGED;
+        } else if (fabs(st->rho) < 1e-30) {         // CG_CHECK_BREAKDOWN(rho)
+            st->done = 1;
+            st->status = ST_STAGNATED;
+        } else {
+            st->beta = tot / st->rho;
+            st->rho = tot;
+            if (it + 1 >= st->max_iter) {
+                st->done = 1;
+                st->status = conv ? ST_CONVERGED : ST_MAX_ITER;  // final check, cg.c:441-443
+            }
+        }
+    }
+}
+
+// Apply the deferred x += alpha p of the last iteration when the reference
+// would have applied it (converged, rho breakdown, max iterations).
+__global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, const double* __restrict__ p0,
+                                                    const double* __restrict__ p1,
+                                                    double* __restrict__ x, const CgState* st) {
+    if (!st->pending || st->iterations <= 0) return;
+    const double alpha = st->alpha;
+    const double* p = ((st->iterations - 1) & 1) ? p1 : p0;
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) x[idx] += alpha * p[idx];
+    }
+}
+
+// Fixed-iteration CG microbenchmark variants: same sweeps, no early exit.
+// (They reuse k_cg_sweep_a / k_cg_sweep_b with max_iter set huge and the
+// convergence test disabled by a zero tolerance.)
+
+// ---------------------------------------------------------------------------
+// Boundary conditions as pure gathers from interior cells (race-free):
+//   Neumann  (boundary_conditions_core_impl.h:41-85): c -> clamp(c, 1, n-2)
+//   Periodic (:90-134):                               0 -> n-2, n-1 -> 1
+// The reference applies x faces, then y faces, then z faces in place; the
+// composition of those copies is exactly this per-coordinate map, edges and
+// corners included. Dirichlet (:139-186) keeps the z > y > x face precedence.
+// Threads cover the boundary shell: z faces (3-D) plus the x/y ring of every
+// plane. mode: 0 Neumann, 1 periodic, 2 Dirichlet.
+// ---------------------------------------------------------------------------
+struct DirVals {
+    double left, right, top, bottom, front, back;
+};
+
+__device__ __forceinline__ int bc_map(int c, int n, int mode) {
+    if (mode == 0) return c == 0 ? 1 : (c == n - 1 ? n - 2 : c);
+    return c == 0 ? n - 2 : (c == n - 1 ? 1 : c);
+}
+
+__global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f, int mode,
+                                                  DirVals dv) {
+    const bool is3d = g.nz > 1;
+    const long long ring = 2LL * g.nx + 2LL * (g.ny - 2);  // x/y boundary ring of one plane
+    const long long nring = ring * g.nz;
+    const long long nzf = is3d ? 2LL * g.nx * g.ny : 0;    // two full z planes
+    const long long total = nring + nzf;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        int i, j, k;
+        if (e < nring) {
+            k = (int)(e / ring);
+            long long q = e % ring;
+            if (q < g.nx) { i = (int)q; j = 0; }
+            else if (q < 2LL * g.nx) { i = (int)(q - g.nx); j = g.ny - 1; }
+            else if (q < 2LL * g.nx + (g.ny - 2)) { i = 0; j = (int)(q - 2LL * g.nx) + 1; }
+            else { i = g.nx - 1; j = (int)(q - 2LL * g.nx - (g.ny - 2)) + 1; }
+        } else {
+            long long q = e - nring;
+            long long plane = (long long)g.nx * g.ny;
+            k = (q < plane) ? 0 : g.nz - 1;
+            q = q % plane;
+            j = (int)(q / g.nx);
+            i = (int)(q % g.nx);
+        }
+        const long long dst = cidx(g, i, j, k);
+        if (mode == 2) {
+            double v;
+            if (is3d && k == 0) v = dv.back;
+            else if (is3d && k == g.nz - 1) v = dv.front;
+            else if (j == 0) v = dv.bottom;
+            else if (j == g.ny - 1) v = dv.top;
+            else if (i == 0) v = dv.left;
+            else v = dv.right;
+            f[dst] = v;
+        } else {
+            int si = bc_map(i, g.nx, mode), sj = bc_map(j, g.ny, mode);
+            int sk = is3d ? bc_map(k, g.nz, mode) : k;
+            f[dst] = f[cidx(g, si, sj, sk)];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Predictor (solver_projection.c:116-185) fused with the boundary copy
+// (boundary_copy_utils.h:93-148): interior cells get
+//   u* = clamp(u + dt((-(u.grad)u + nu lap u) + s)),
+// boundary cells get u* = u (u_star starts as a copy of u and its faces are
+// then restored from u, so the boundary of u* is always u's).
+// Source term s: per-row / per-column tables computed on the host with the
+// reference's libm expression (compute_source_terms at iter = 0), plus
+// Boussinesq buoyancy (energy_solver.c:185-196) when beta != 0.
+// ---------------------------------------------------------------------------
+struct PredCoef {
+    double two_dx, two_dy, inv_2dz;   // first derivatives
+    double dx_sq, dy_sq, inv_dz2;     // second derivatives
+    double dt, nu;
+    double beta, T_ref, g0, g1, g2;
+};
+
+template <bool BUOY>
+__global__ __launch_bounds__(256) void k_predictor(Geo g, PredCoef pc,
+                                                   const double* __restrict__ U,
+                                                   const double* __restrict__ V,
+                                                   const double* __restrict__ W,
+                                                   const double* __restrict__ T,
+                                                   const double* __restrict__ src_u_row,
+                                                   const double* __restrict__ src_v_col,
+                                                   double* __restrict__ us,
+                                                   double* __restrict__ vs,
+                                                   double* __restrict__ ws) {
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    if (i >= g.nx || j >= g.ny) return;
+    const long long idx = cidx(g, i, j, k);
+    const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
+                           k >= g.k0 && k < g.k1);
+    if (!interior) {
+        us[idx] = U[idx];
+        vs[idx] = V[idx];
+        ws[idx] = W[idx];
+        return;
+    }
+    const long long px = g.px, sz = g.sz;
+    double u = U[idx], v = V[idx], w = W[idx];
+    double du_dx = (U[idx + 1] - U[idx - 1]) / pc.two_dx;
+    double du_dy = (U[idx + px] - U[idx - px]) / pc.two_dy;
+    double du_dz = (U[idx + sz] - U[idx - sz]) * pc.inv_2dz;
+    double dv_dx = (V[idx + 1] - V[idx - 1]) / pc.two_dx;
+    double dv_dy = (V[idx + px] - V[idx - px]) / pc.two_dy;
+    double dv_dz = (V[idx + sz] - V[idx - sz]) * pc.inv_2dz;
+    double dw_dx = (W[idx + 1] - W[idx - 1]) / pc.two_dx;
+    double dw_dy = (W[idx + px] - W[idx - px]) / pc.two_dy;
+    double dw_dz = (W[idx + sz] - W[idx - sz]) * pc.inv_2dz;
+    double conv_u = u * du_dx + v * du_dy + w * du_dz;
+    double conv_v = u * dv_dx + v * dv_dy + w * dv_dz;
+    double conv_w = u * dw_dx + v * dw_dy + w * dw_dz;
+    double d2u_dx2 = (U[idx + 1] - 2.0 * u + U[idx - 1]) / pc.dx_sq;
+    double d2u_dy2 = (U[idx + px] - 2.0 * u + U[idx - px]) / pc.dy_sq;
+    double d2u_dz2 = (U[idx + sz] - 2.0 * u + U[idx - sz]) * pc.inv_dz2;
+    double d2v_dx2 = (V[idx + 1] - 2.0 * v + V[idx - 1]) / pc.dx_sq;
+    double d2v_dy2 = (V[idx + px] - 2.0 * v + V[idx - px]) / pc.dy_sq;
+    double d2v_dz2 = (V[idx + sz] - 2.0 * v + V[idx - sz]) * pc.inv_dz2;
+    double d2w_dx2 = (W[idx + 1] - 2.0 * w + W[idx - 1]) / pc.dx_sq;
+    double d2w_dy2 = (W[idx + px] - 2.0 * w + W[idx - px]) / pc.dy_sq;
+    double d2w_dz2 = (W[idx + sz] - 2.0 * w + W[idx - sz]) * pc.inv_dz2;
+    double visc_u = pc.nu * (d2u_dx2 + d2u_dy2 + d2u_dz2);
+    double visc_v = pc.nu * (d2v_dx2 + d2v_dy2 + d2v_dz2);
+    double visc_w = pc.nu * (d2w_dx2 + d2w_dy2 + d2w_dz2);
+    double su = src_u_row[j];
+    double sv = src_v_col[i];
+    double sw = 0.0;
+    if (BUOY) {
+        double dT = T[idx] - pc.T_ref;
+        su += -pc.beta * dT * pc.g0;
+        sv += -pc.beta * dT * pc.g1;
+        sw += -pc.beta * dT * pc.g2;
+    }
+    double a = u + pc.dt * (-conv_u + visc_u + su);
+    double b = v + pc.dt * (-conv_v + visc_v + sv);
+    double c = w + pc.dt * (-conv_w + visc_w + sw);
+    us[idx] = fmax(-100.0, fmin(100.0, a));
+    vs[idx] = fmax(-100.0, fmin(100.0, b));
+    ws[idx] = fmax(-100.0, fmin(100.0, c));
+}
+
+// ---------------------------------------------------------------------------
+// Corrector (solver_projection.c:230-250) + boundary restore (:277-278) +
+// NaN/Inf scan (:281-289) + stats (solver_registry.c:31-49), one pass.
+// Interior: u = clamp(u* - (dt/rho) grad p). Boundary cells keep u (== u*).
+// Every cell contributes to max |u| and max |p| and the non-finite flag.
+// red[0] = encoded max velocity, red[1] = encoded max |p|, red[2] = nonfinite.
+// ---------------------------------------------------------------------------
+struct CorrCoef {
+    double two_dx, two_dy, inv_2dz;
+    double dt_over_rho;
+};
+
+__global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
+                                                   const double* __restrict__ us,
+                                                   const double* __restrict__ vs,
+                                                   const double* __restrict__ ws,
+                                                   const double* __restrict__ P,
+                                                   double* __restrict__ U, double* __restrict__ V,
+                                                   double* __restrict__ W,
+                                                   unsigned long long* red) {
+    __shared__ double shv[4], shp[4];
+    __shared__ int shbad;
+    if (threadIdx.x == 0) shbad = 0;
+    __syncthreads();
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    double mv = 0.0, mp = 0.0;
+    if (i < g.nx && j < g.ny) {
+        const long long idx = cidx(g, i, j, k);
+        const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
+                               k >= g.k0 && k < g.k1);
+        double u, v, w;
+        if (interior) {
+            double dp_dx = (P[idx + 1] - P[idx - 1]) / cc.two_dx;
+            double dp_dy = (P[idx + g.px] - P[idx - g.px]) / cc.two_dy;
+            double dp_dz = (P[idx + g.sz] - P[idx - g.sz]) * cc.inv_2dz;
+            u = us[idx] - cc.dt_over_rho * dp_dx;
+            v = vs[idx] - cc.dt_over_rho * dp_dy;
+            w = ws[idx] - cc.dt_over_rho * dp_dz;
+            u = fmax(-100.0, fmin(100.0, u));
+            v = fmax(-100.0, fmin(100.0, v));
+            w = fmax(-100.0, fmin(100.0, w));
+            U[idx] = u;
+            V[idx] = v;
+            W[idx] = w;
+        } else {
+            u = U[idx];
+            v = V[idx];
+            w = W[idx];
+        }
+        double p = P[idx];
+        if (!isfinite(u) || !isfinite(v) || !isfinite(w) || !isfinite(p)) shbad = 1;
+        double vel = sqrt((u * u) + (v * v) + (w * w));
+        if (vel > mv) mv = vel;
+        double ap = fabs(p);
+        if (ap > mp) mp = ap;
+    }
+    mv = wave_max(mv);
+    mp = wave_max(mp);
+    if ((threadIdx.x & 63) == 0) {
+        shv[threadIdx.x >> 6] = mv;
+        shp[threadIdx.x >> 6] = mp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = fmax(fmax(shv[0], shv[1]), fmax(shv[2], shv[3]));
+        double b = fmax(fmax(shp[0], shp[1]), fmax(shp[2], shp[3]));
+        atomicMax(&red[0], ord_enc(a));
+        atomicMax(&red[1], ord_enc(b));
+        if (shbad) atomicOr(&red[2], 1ull);
+    }
+}
+
+// Max over a full field (stats: max temperature, solver_registry.c:52-62).
+__global__ __launch_bounds__(256) void k_field_max(Geo g, const double* __restrict__ f,
+                                                   unsigned long long* out) {
+    __shared__ double sh[4];
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    double m = -INFINITY;
+    if (i < g.nx && j < g.ny) {
+        double v = f[cidx(g, i, j, k)];
+        if (!isnan(v)) m = v;
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
+        atomicMax(out, ord_enc(a));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Relaxation solvers.
+// Red-Black SOR colour pass (linear_solver_redblack.c:97-133). `parity` is the
+// (i+j+k) parity updated in this pass: the reference's first ("red") pass
+// updates odd cells, the second even cells. Each cell reads only the other
+// colour, so the in-place update is race-free and bitwise the reference's.
+// Jacobi (linear_solver_jacobi.c:92-109) reads xin, writes xout.
+// ---------------------------------------------------------------------------
+struct RelaxCoef {
+    double dx2, dy2, inv_dz2, inv_factor, omega;
+};
+
+__global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __restrict__ x,
+                                                const double* __restrict__ rhs, int parity) {
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            if (((c.i + c.j + k) & 1) != parity) continue;
+            double pn = -(rhs[idx] - (x[idx + 1] + x[idx - 1]) / rc.dx2 -
+                          (x[idx + g.px] + x[idx - g.px]) / rc.dy2 -
+                          (x[idx + g.sz] + x[idx - g.sz]) * rc.inv_dz2) *
+                        rc.inv_factor;
+            double xo = x[idx];
+            x[idx] = xo + rc.omega * (pn - xo);
+        }
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_jacobi(Geo g, RelaxCoef rc, const double* __restrict__ xin,
+                                               double* __restrict__ xout,
+                                               const double* __restrict__ rhs) {
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            xout[idx] = -(rhs[idx] - (xin[idx + 1] + xin[idx - 1]) / rc.dx2 -
+                          (xin[idx + g.px] + xin[idx - g.px]) / rc.dy2 -
+                          (xin[idx + g.sz] + xin[idx - g.sz]) * rc.inv_dz2) *
+                         rc.inv_factor;
+        }
+    }
+}
+
+// L-infinity residual |lap(x) - rhs| (linear_solver.c:304-346, division form).
+struct ResCoef {
+    double dx2, dy2, inv_dz2;
+};
+
+__global__ __launch_bounds__(NT) void k_residual_linf(Geo g, ResCoef rc,
+                                                      const double* __restrict__ x,
+                                                      const double* __restrict__ rhs,
+                                                      unsigned long long* out) {
+    __shared__ double sh[NWAVE];
+    double m = 0.0;
+    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        TileCoord c = tile_coord(g, t);
+        if (!c.active) continue;
+        long long idx = cidx(g, c.i, c.j, c.kb);
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            double lap = (x[idx + 1] - 2.0 * x[idx] + x[idx - 1]) / rc.dx2 +
+                         (x[idx + g.px] - 2.0 * x[idx] + x[idx - g.px]) / rc.dy2 +
+                         (x[idx + g.sz] + x[idx - g.sz] - 2.0 * x[idx]) * rc.inv_dz2;
+            double res = fabs(lap - rhs[idx]);
+            if (res > m) m = res;
+        }
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = sh[0];
+        for (int w = 1; w < NWAVE; ++w) a = fmax(a, sh[w]);
+        atomicMax(out, ord_enc(a));
+    }
+}
+
+}  // namespace cfdhip

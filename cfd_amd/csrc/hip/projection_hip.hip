@@ -1,0 +1,963 @@
+// projection_hip.hip -- device context and step orchestration behind the
+// C-ABI of include/cfd_hip/projection_hip.h.
+//
+// One context = one device, one HIP stream, all fields resident in HBM with a
+// padded row pitch. A step is: predictor -> (p_new = p) -> pressure solve on
+// p_new with the divergence right-hand side fused into the CG setup ->
+// corrector + boundary restore + NaN scan + stats -> swap(p, p_new).
+// The CG loop keeps alpha/beta/convergence on the device (CgState) and the
+// host only polls a pinned copy of the state every few iterations, so there
+// is no host round trip per iteration (the reference GPU path does two per
+// iteration, poisson_cg_gpu_solve.cuh:189-203).
+#include "kernels.hpp"
+
+#include "cfd_hip/projection_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace cfdhip;
+
+// Error reporting goes through the host library's thread-local error state
+// (cfd_set_error, logging.c:39-46 in the reference). Weak, so the library
+// links against either the reference's host library or ours.
+extern "C" void cfd_set_error(cfd_status_t status, const char* message) __attribute__((weak));
+
+static void set_err(cfd_status_t s, const char* msg) {
+    if (cfd_set_error) cfd_set_error(s, msg);
+}
+
+#define HIP_TRY(call)                                                              \
+    do {                                                                           \
+        hipError_t e_ = (call);                                                    \
+        if (e_ != hipSuccess) {                                                    \
+            char buf_[256];                                                        \
+            snprintf(buf_, sizeof(buf_), "HIP error %s at %s:%d (%s)",             \
+                     hipGetErrorString(e_), __FILE__, __LINE__, #call);            \
+            set_err(CFD_ERROR, buf_);                                              \
+            return CFD_ERROR;                                                      \
+        }                                                                          \
+    } while (0)
+
+namespace {
+
+struct TimedLaunch {
+    hipEvent_t a, b;
+    int kind;
+};
+
+}  // namespace
+
+struct hip_proj_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    size_t nx = 0, ny = 0, nz = 0;
+    long long px = 0, ps = 0;
+    Geo geo{};
+    int grid_cap = 2048;
+    hip_proj_config_t cfg{};
+    // fields
+    double *u = nullptr, *v = nullptr, *w = nullptr, *p = nullptr, *T = nullptr;
+    double *us = nullptr, *vs = nullptr, *ws = nullptr, *pn = nullptr;
+    double *r = nullptr, *pa = nullptr, *pb = nullptr;
+    double *rhs = nullptr, *xt = nullptr;
+    double *src_u_row = nullptr, *src_v_col = nullptr;
+    std::vector<double> h_src_u, h_src_v;
+    // reductions / state
+    CgState* st = nullptr;
+    double* partials = nullptr;
+    unsigned* counter = nullptr;
+    unsigned long long* red = nullptr;   // [0] max vel, [1] max |p|, [2] nonfinite, [3] max T, [4] residual
+    CgState* h_state = nullptr;          // pinned, 2 slots + final
+    unsigned long long* h_red = nullptr; // pinned, 8
+    hipEvent_t ev_poll[2] = {nullptr, nullptr};
+    double rho0 = 1.0;
+    double max_T = 0.0;
+    int have_T = 0;
+    poisson_solver_stats_t pstats{};
+    size_t bytes = 0;
+    // timing
+    int timing = 0;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<TimedLaunch> pending;
+    double kt_ms[HIP_KT_COUNT] = {0};
+    long long kt_n[HIP_KT_COUNT] = {0};
+};
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+static cfd_status_t dalloc(hip_proj_ctx* c, double** ptr, size_t n) {
+    HIP_TRY(hipMalloc((void**)ptr, n * sizeof(double)));
+    HIP_TRY(hipMemsetAsync(*ptr, 0, n * sizeof(double), c->stream));
+    c->bytes += n * sizeof(double);
+    return CFD_SUCCESS;
+}
+
+static size_t field_elems(const hip_proj_ctx* c) { return (size_t)c->ps * c->nz; }
+
+static double* field_ptr(hip_proj_ctx* c, int id) {
+    switch (id) {
+        case HIP_FIELD_U: return c->u;
+        case HIP_FIELD_V: return c->v;
+        case HIP_FIELD_W: return c->w;
+        case HIP_FIELD_P: return c->p;
+        case HIP_FIELD_T: return c->T;
+        default: return nullptr;
+    }
+}
+
+static hipEvent_t take_event(hip_proj_ctx* c) {
+    if (c->ev_used == c->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+}
+
+static void flush_timing(hip_proj_ctx* c) {
+    for (auto& t : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+            c->kt_ms[t.kind] += ms;
+            c->kt_n[t.kind] += 1;
+        }
+    }
+    c->pending.clear();
+    c->ev_used = 0;
+}
+
+// Record events around a launch when timing is enabled. The pool is flushed
+// at every host synchronisation point.
+template <typename F>
+static void timed(hip_proj_ctx* c, int kind, F&& launch) {
+    if (!c->timing) {
+        launch();
+        return;
+    }
+    hipEvent_t a = take_event(c), b = take_event(c);
+    if (!a || !b) {
+        launch();
+        return;
+    }
+    hipEventRecord(a, c->stream);
+    launch();
+    hipEventRecord(b, c->stream);
+    c->pending.push_back({a, b, kind});
+}
+
+static int tile_grid(const hip_proj_ctx* c) {
+    long long nt = (long long)c->geo.tiles_x * c->geo.tiles_y * c->geo.tiles_z;
+    return (int)std::max(1LL, std::min<long long>(nt, c->grid_cap));
+}
+
+static dim3 cell_grid(const hip_proj_ctx* c) {
+    return dim3((unsigned)((c->nx + 63) / 64), (unsigned)((c->ny + 3) / 4), (unsigned)c->nz);
+}
+
+static unsigned shell_blocks(const hip_proj_ctx* c) {
+    long long ring = 2LL * c->nx + 2LL * (c->ny - 2);
+    long long total = ring * (long long)c->nz + (c->nz > 1 ? 2LL * c->nx * c->ny : 0);
+    long long b = (total + 255) / 256;
+    return (unsigned)std::max(1LL, std::min(b, 65535LL));
+}
+
+static void launch_bc(hip_proj_ctx* c, double* f, int mode, const DirVals& dv) {
+    hipLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->geo, f,
+                       mode, dv);
+}
+
+static __global__ void k_init_red(unsigned long long* red) {
+    if (threadIdx.x == 0) {
+        red[0] = 0x8000000000000000ull;  // enc(+0.0): reference maxima start at 0.0
+        red[1] = 0x8000000000000000ull;
+        red[2] = 0ull;
+        red[3] = 0x000FFFFFFFFFFFFFull;  // enc(-inf)
+        red[4] = 0x8000000000000000ull;
+    }
+}
+
+static double ord_dec(unsigned long long e) {
+    unsigned long long b = (e & 0x8000000000000000ull) ? (e & 0x7FFFFFFFFFFFFFFFull) : ~e;
+    double d;
+    memcpy(&d, &b, sizeof(d));
+    return d;
+}
+
+static Lap make_lap(double dx, double dy, double dz) {
+    Lap L;
+    L.dx2_inv = 1.0 / (dx * dx);
+    L.dy2_inv = 1.0 / (dy * dy);
+    L.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
+    return L;
+}
+
+// ---------------------------------------------------------------------------
+// pressure solvers on ctx->pn
+// ---------------------------------------------------------------------------
+enum RhsSource { RHS_FROM_VELOCITY, RHS_FROM_ARRAY };
+
+static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
+                             const DivCoef& dc, RhsSource src, double rel_tol, double abs_tol,
+                             int max_iter, int check_interval, bool final_bc) {
+    const Lap L = make_lap(dx, dy, dz);
+    const int G = tile_grid(c);
+    const DirVals dv{};
+    double* x = c->pn;
+    // poisson_solver_apply_bc(x) at solve start (linear_solver_cg.c:320)
+    launch_bc(c, x, 0, dv);
+    timed(c, HIP_KT_CG_SETUP, [&] {
+        if (src == RHS_FROM_VELOCITY)
+            hipLaunchKernelGGL((k_cg_setup<true, false, true>), dim3(G), dim3(NT), 0, c->stream,
+                               c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x, c->r, c->st,
+                               c->partials, c->counter, rel_tol, abs_tol, max_iter,
+                               check_interval);
+        else
+            hipLaunchKernelGGL((k_cg_setup<false, false, true>), dim3(G), dim3(NT), 0,
+                               c->stream, c->geo, L, dc, nullptr, nullptr, nullptr, c->rhs, x,
+                               c->r, c->st, c->partials, c->counter, rel_tol, abs_tol, max_iter,
+                               check_interval);
+    });
+    double* P[2] = {c->pa, c->pb};
+    int it = 0;
+    if (max_iter > 0) {
+        timed(c, HIP_KT_CG_SWEEP_A, [&] {
+            hipLaunchKernelGGL(k_cg_sweep_a<true>, dim3(G), dim3(NT), 0, c->stream, c->geo, L,
+                               c->r, P[1], P[0], x, c->st, c->partials, c->counter, 0);
+        });
+        timed(c, HIP_KT_CG_SWEEP_B, [&] {
+            hipLaunchKernelGGL(k_cg_sweep_b, dim3(G), dim3(NT), 0, c->stream, c->geo, L, P[0],
+                               c->r, c->st, c->partials, c->counter, 0);
+        });
+        it = 1;
+    }
+    int chunk = 8;
+    const int chunk_max = std::max(1, c->cfg.poll_interval);
+    int slot = 0, prev = -1;
+    while (it < max_iter) {
+        const int n = std::min(chunk, max_iter - it);
+        for (int q = 0; q < n; ++q, ++it) {
+            double* pnew = P[it & 1];
+            double* pold = P[(it + 1) & 1];
+            timed(c, HIP_KT_CG_SWEEP_A, [&] {
+                hipLaunchKernelGGL(k_cg_sweep_a<false>, dim3(G), dim3(NT), 0, c->stream, c->geo,
+                                   L, c->r, pold, pnew, x, c->st, c->partials, c->counter, it);
+            });
+            timed(c, HIP_KT_CG_SWEEP_B, [&] {
+                hipLaunchKernelGGL(k_cg_sweep_b, dim3(G), dim3(NT), 0, c->stream, c->geo, L,
+                                   pnew, c->r, c->st, c->partials, c->counter, it);
+            });
+        }
+        HIP_TRY(hipMemcpyAsync(&c->h_state[slot], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
+        if (prev >= 0) {
+            HIP_TRY(hipEventSynchronize(c->ev_poll[prev]));
+            if (c->h_state[prev].done) break;
+        }
+        prev = slot;
+        slot ^= 1;
+        chunk = std::min(chunk * 2, chunk_max);
+    }
+    hipLaunchKernelGGL(k_cg_finalize, dim3(G), dim3(NT), 0, c->stream, c->geo, P[0], P[1], x,
+                       c->st);
+    HIP_TRY(hipMemcpyAsync(&c->h_state[2], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    flush_timing(c);
+    const CgState& s = c->h_state[2];
+    const bool stagnated = (s.status == ST_STAGNATED);
+    // final poisson_solver_apply_bc (cg.c:447); the breakdown exit skips it.
+    if (final_bc && !stagnated && !(s.iterations == 0 && s.status == ST_CONVERGED))
+        launch_bc(c, x, 0, dv);
+    c->pstats.status = (poisson_solver_status_t)s.status;
+    c->pstats.iterations = s.iterations;
+    c->pstats.initial_residual = s.res0;
+    c->pstats.final_residual = s.res;
+    return (s.status == ST_CONVERGED) ? CFD_SUCCESS : CFD_ERROR_MAX_ITER;
+}
+
+static double optimal_omega(size_t nx, size_t ny, size_t nz, double dx, double dy, double dz) {
+    // linear_solver_internal.h:184-220
+    double inv_dx2 = 1.0 / (dx * dx), inv_dy2 = 1.0 / (dy * dy);
+    double inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
+    double num = cos(M_PI / (double)(nx - 1)) * inv_dx2 + cos(M_PI / (double)(ny - 1)) * inv_dy2;
+    double den = inv_dx2 + inv_dy2;
+    if (nz > 1 && inv_dz2 > 0.0) {
+        num += cos(M_PI / (double)(nz - 1)) * inv_dz2;
+        den += inv_dz2;
+    }
+    double rj = num / den;
+    return 2.0 / (1.0 + sqrt(1.0 - (rj * rj)));
+}
+
+static cfd_status_t residual_linf(hip_proj_ctx* c, const double* x, const ResCoef& rc, double* out) {
+    const int G = tile_grid(c);
+    hipLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->red);
+    timed(c, HIP_KT_RESIDUAL, [&] {
+        hipLaunchKernelGGL(k_residual_linf, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, x, c->rhs,
+                           c->red + 4);
+    });
+    HIP_TRY(hipMemcpyAsync(c->h_red, c->red, 8 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *out = ord_dec(c->h_red[4]);
+    return CFD_SUCCESS;
+}
+
+// Relaxation methods driven by the common loop (linear_solver.c:397-485):
+// L-infinity residual before the loop and every check_interval iterations.
+static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double dy, double dz,
+                                double rel_tol, double abs_tol, int max_iter, int check_interval,
+                                double omega_in) {
+    const int G = tile_grid(c);
+    RelaxCoef rc;
+    rc.dx2 = dx * dx;
+    rc.dy2 = dy * dy;
+    rc.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
+    rc.inv_factor = 1.0 / (2.0 * (1.0 / rc.dx2 + 1.0 / rc.dy2 + rc.inv_dz2));
+    rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nz, dx, dy, dz) : omega_in;
+    ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
+    const DirVals dv{};
+    double res0 = 0.0;
+    cfd_status_t s = residual_linf(c, c->pn, res_c, &res0);
+    if (s != CFD_SUCCESS) return s;
+    double tol = rel_tol * res0;
+    if (tol < abs_tol) tol = abs_tol;
+    c->pstats.initial_residual = res0;
+    if (res0 < abs_tol) {
+        c->pstats.status = POISSON_CONVERGED;
+        c->pstats.iterations = 0;
+        c->pstats.final_residual = res0;
+        return CFD_SUCCESS;
+    }
+    int iter;
+    bool conv = false;
+    double res = res0;
+    for (iter = 0; iter < max_iter; ++iter) {
+        if (method == HIP_POISSON_REDBLACK) {
+            timed(c, HIP_KT_RELAX, [&] {
+                hipLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
+                                   c->rhs, 1);
+            });
+            timed(c, HIP_KT_RELAX, [&] {
+                hipLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
+                                   c->rhs, 0);
+            });
+        } else {
+            timed(c, HIP_KT_RELAX, [&] {
+                hipLaunchKernelGGL(k_jacobi, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
+                                   c->xt, c->rhs);
+            });
+            // memcpy(x, x_temp) + BC == swap buffers then BC (all boundary
+            // cells are rewritten by the Neumann gather)
+            std::swap(c->pn, c->xt);
+        }
+        launch_bc(c, c->pn, 0, dv);
+        if (iter % check_interval == 0) {
+            s = residual_linf(c, c->pn, res_c, &res);
+            if (s != CFD_SUCCESS) return s;
+            if (res < tol || res < abs_tol) {
+                conv = true;
+                break;
+            }
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    flush_timing(c);
+    c->pstats.iterations = iter + 1;
+    c->pstats.final_residual = res;
+    c->pstats.status = conv ? POISSON_CONVERGED : POISSON_MAX_ITER;
+    return conv ? CFD_SUCCESS : CFD_ERROR_MAX_ITER;
+}
+
+static cfd_status_t ensure_aux(hip_proj_ctx* c, bool need_rhs, bool need_xt) {
+    const size_t n = field_elems(c);
+    if (need_rhs && !c->rhs) {
+        cfd_status_t s = dalloc(c, &c->rhs, n);
+        if (s != CFD_SUCCESS) return s;
+    }
+    if (need_xt && !c->xt) {
+        cfd_status_t s = dalloc(c, &c->xt, n);
+        if (s != CFD_SUCCESS) return s;
+    }
+    return CFD_SUCCESS;
+}
+
+static cfd_status_t validate_params(const hip_proj_ctx* c, const grid* g,
+                                    const ns_solver_params_t* prm) {
+    if (!g || !prm) return CFD_ERROR_INVALID;
+    if (g->nx != c->nx || g->ny != c->ny || g->nz != c->nz) {
+        set_err(CFD_ERROR_INVALID, "projection_hip: grid does not match the context");
+        return CFD_ERROR_INVALID;
+    }
+    if (c->nz > 1 && g->dz) {
+        for (size_t k = 1; k < c->nz - 1; k++)
+            if (fabs(g->dz[k] - g->dz[0]) > 1e-14) {  // solver_projection.c:59-66
+                set_err(CFD_ERROR_INVALID, "projection_hip: non-uniform dz");
+                return CFD_ERROR_INVALID;
+            }
+    }
+    if (prm->source_func) {
+        set_err(CFD_ERROR_UNSUPPORTED,
+                "projection_hip: host source_func callbacks cannot run on the device");
+        return CFD_ERROR_UNSUPPORTED;
+    }
+    if (prm->alpha > 0.0) {
+        set_err(CFD_ERROR_UNSUPPORTED, "projection_hip: energy equation not enabled in this build");
+        return CFD_ERROR_UNSUPPORTED;
+    }
+    return CFD_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+hip_proj_config_t hip_proj_config_default(void) {
+    hip_proj_config_t c;
+    memset(&c, 0, sizeof(c));
+    c.device = -1;
+    c.poisson_method = HIP_POISSON_CG;
+    c.poisson_tolerance = 1e-6;
+    c.poisson_abs_tolerance = 1e-10;
+    c.poisson_max_iter = 5000;
+    c.poisson_check_interval = 1;
+    c.sor_omega = 0.0;
+    c.poll_interval = 64;
+    c.kchunk = 0;
+    c.verbose = 0;
+    return c;
+}
+
+int hip_projection_available(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n > 0 ? 1 : 0;
+}
+
+static void free_ctx(hip_proj_ctx* c) {
+    if (!c) return;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    double* bufs[] = {c->u,  c->v,  c->w,   c->p,  c->T,   c->us,       c->vs,       c->ws,
+                      c->pn, c->r,  c->pa,  c->pb, c->rhs, c->xt, c->src_u_row, c->src_v_col};
+    for (double* b : bufs)
+        if (b) hipFree(b);
+    if (c->st) hipFree(c->st);
+    if (c->partials) hipFree(c->partials);
+    if (c->counter) hipFree(c->counter);
+    if (c->red) hipFree(c->red);
+    if (c->h_state) hipHostFree(c->h_state);
+    if (c->h_red) hipHostFree(c->h_red);
+    for (int i = 0; i < 2; i++)
+        if (c->ev_poll[i]) hipEventDestroy(c->ev_poll[i]);
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+    c->grid_cap = std::max(64, prop.multiProcessorCount * 8);
+    c->nx = nx;
+    c->ny = ny;
+    c->nz = nz;
+    c->px = (long long)((nx + 7) / 8 * 8);
+    c->ps = c->px * (long long)ny;
+    Geo& g = c->geo;
+    g.nx = (int)nx;
+    g.ny = (int)ny;
+    g.nz = (int)nz;
+    g.px = c->px;
+    g.ps = c->ps;
+    g.sz = (nz > 1) ? c->ps : 0;
+    g.k0 = (nz > 1) ? 1 : 0;
+    g.k1 = (nz > 1) ? (int)nz - 1 : 1;
+    const int nint_k = g.k1 - g.k0;
+    int kc = c->cfg.kchunk;
+    if (kc <= 0) {
+        // enough tiles to fill every CU several times, long z runs otherwise
+        long long xy_tiles = (long long)((nx + TX - 1) / TX) * (long long)((ny + TY - 1) / TY);
+        long long want = 4LL * c->grid_cap;
+        kc = (int)std::max<long long>(8, (xy_tiles * nint_k + want - 1) / want);
+        kc = std::min(kc, std::max(1, nint_k));
+    }
+    g.kc = std::max(1, kc);
+    g.tiles_x = (int)((nx + TX - 1) / TX);
+    g.tiles_y = (int)((ny + TY - 1) / TY);
+    g.tiles_z = (nint_k + g.kc - 1) / g.kc;
+
+    const size_t n = field_elems(c);
+    double** fields[] = {&c->u, &c->v, &c->w, &c->p, &c->us, &c->vs, &c->ws, &c->pn,
+                         &c->r, &c->pa, &c->pb};
+    for (double** f : fields) {
+        cfd_status_t s = dalloc(c, f, n);
+        if (s != CFD_SUCCESS) return s;
+    }
+    if (dalloc(c, &c->src_u_row, ny) != CFD_SUCCESS) return CFD_ERROR;
+    if (dalloc(c, &c->src_v_col, nx) != CFD_SUCCESS) return CFD_ERROR;
+    HIP_TRY(hipMalloc((void**)&c->st, sizeof(CgState)));
+    HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
+    HIP_TRY(hipMalloc((void**)&c->partials, sizeof(double) * c->grid_cap));
+    HIP_TRY(hipMalloc((void**)&c->counter, 64));
+    HIP_TRY(hipMemsetAsync(c->counter, 0, 64, c->stream));
+    HIP_TRY(hipMalloc((void**)&c->red, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipHostMalloc((void**)&c->h_state, 3 * sizeof(CgState), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&c->h_red, 8 * sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_poll[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_poll[1], hipEventDisableTiming));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return CFD_SUCCESS;
+}
+
+hip_proj_ctx_t* hip_proj_create(size_t nx, size_t ny, size_t nz, const hip_proj_config_t* cfg) {
+    if (nx < 3 || ny < 3 || nz == 0 || (nz > 1 && nz < 3)) {
+        set_err(CFD_ERROR_INVALID, "projection_hip: grid must be >= 3 points per active axis");
+        return nullptr;
+    }
+    if (!hip_projection_available()) {
+        set_err(CFD_ERROR_UNSUPPORTED, "projection_hip: no HIP device available");
+        return nullptr;
+    }
+    hip_proj_ctx* c = new hip_proj_ctx();
+    c->cfg = cfg ? *cfg : hip_proj_config_default();
+    if (c->cfg.device < 0) {
+        int d = 0;
+        hipGetDevice(&d);
+        c->device = d;
+    } else {
+        c->device = c->cfg.device;
+    }
+    if (c->cfg.poll_interval <= 0) c->cfg.poll_interval = 64;
+    if (init_ctx(c, nx, ny, nz) != CFD_SUCCESS) {
+        free_ctx(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void hip_proj_destroy(hip_proj_ctx_t* ctx) { free_ctx(ctx); }
+
+size_t hip_proj_device_bytes(const hip_proj_ctx_t* ctx) { return ctx ? ctx->bytes : 0; }
+size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx) { return ctx ? (size_t)ctx->px : 0; }
+
+cfd_status_t hip_proj_synchronize(hip_proj_ctx_t* c) {
+    if (!c) return CFD_ERROR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    flush_timing(c);
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_set_field(hip_proj_ctx_t* c, int id, const double* host) {
+    if (!c || !host) return CFD_ERROR_INVALID;
+    double* d = field_ptr(c, id);
+    if (id == HIP_FIELD_T && !d) {
+        if (dalloc(c, &c->T, field_elems(c)) != CFD_SUCCESS) return CFD_ERROR_NOMEM;
+        d = c->T;
+    }
+    if (!d) return CFD_ERROR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy2DAsync(d, c->px * sizeof(double), host, c->nx * sizeof(double),
+                             c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
+                             c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (id == HIP_FIELD_T) c->have_T = 1;
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_get_field(hip_proj_ctx_t* c, int id, double* host) {
+    if (!c || !host) return CFD_ERROR_INVALID;
+    double* d = field_ptr(c, id);
+    if (!d) return CFD_ERROR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy2DAsync(host, c->nx * sizeof(double), d, c->px * sizeof(double),
+                             c->nx * sizeof(double), c->ny * c->nz, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return CFD_SUCCESS;
+}
+
+static __global__ void k_fill(double* f, long long n, double v) {
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x)
+        f[e] = v;
+}
+
+cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
+    if (!c) return CFD_ERROR_INVALID;
+    double* d = field_ptr(c, id);
+    if (id == HIP_FIELD_T && !d) {
+        if (dalloc(c, &c->T, field_elems(c)) != CFD_SUCCESS) return CFD_ERROR_NOMEM;
+        d = c->T;
+        c->have_T = 1;
+    }
+    if (!d) return CFD_ERROR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, c->stream, d,
+                       (long long)field_elems(c), value);
+    HIP_TRY(hipGetLastError());
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_set_density(hip_proj_ctx_t* c, double rho0) {
+    if (!c) return CFD_ERROR_INVALID;
+    c->rho0 = rho0;
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_upload(hip_proj_ctx_t* c, const flow_field* f) {
+    if (!c || !f) return CFD_ERROR_INVALID;
+    if (f->nx != c->nx || f->ny != c->ny || f->nz != c->nz) return CFD_ERROR_INVALID;
+    cfd_status_t s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_V, f->v)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_W, f->w)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_P, f->p)) != CFD_SUCCESS) return s;
+    if (f->T) {
+        if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
+        size_t n = c->nx * c->ny * c->nz;
+        double m = f->T[0];
+        for (size_t i = 1; i < n; i++)
+            if (f->T[i] > m) m = f->T[i];
+        c->max_T = m;
+    }
+    c->rho0 = f->rho ? f->rho[0] : 1.0;
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_download(hip_proj_ctx_t* c, flow_field* f) {
+    if (!c || !f) return CFD_ERROR_INVALID;
+    cfd_status_t s;
+    if ((s = hip_proj_get_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_get_field(c, HIP_FIELD_V, f->v)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_get_field(c, HIP_FIELD_W, f->w)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_get_field(c, HIP_FIELD_P, f->p)) != CFD_SUCCESS) return s;
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type) {
+    if (!c) return CFD_ERROR_INVALID;
+    double* d = field_ptr(c, id);
+    if (!d) return CFD_ERROR_INVALID;
+    int mode;
+    if (type == BC_TYPE_NEUMANN) mode = 0;
+    else if (type == BC_TYPE_PERIODIC) mode = 1;
+    else {
+        set_err(CFD_ERROR_UNSUPPORTED, "hip_proj_apply_scalar_bc: only NEUMANN and PERIODIC");
+        return CFD_ERROR_UNSUPPORTED;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    launch_bc(c, d, mode, DirVals{});
+    HIP_TRY(hipGetLastError());
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* c, int id, const bc_dirichlet_values_t* v) {
+    if (!c || !v) return CFD_ERROR_INVALID;
+    double* d = field_ptr(c, id);
+    if (!d) return CFD_ERROR_INVALID;
+    DirVals dv{v->left, v->right, v->top, v->bottom, v->front, v->back};
+    HIP_TRY(hipSetDevice(c->device));
+    launch_bc(c, d, 2, dv);
+    HIP_TRY(hipGetLastError());
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_get_poisson_stats(hip_proj_ctx_t* c, poisson_solver_stats_t* s) {
+    if (!c || !s) return CFD_ERROR_INVALID;
+    *s = c->pstats;
+    return CFD_SUCCESS;
+}
+
+void hip_proj_enable_timing(hip_proj_ctx_t* c, int enable) {
+    if (c) c->timing = enable ? 1 : 0;
+}
+
+void hip_proj_reset_timing(hip_proj_ctx_t* c) {
+    if (!c) return;
+    hipStreamSynchronize(c->stream);
+    flush_timing(c);
+    for (int k = 0; k < HIP_KT_COUNT; k++) {
+        c->kt_ms[k] = 0;
+        c->kt_n[k] = 0;
+    }
+}
+
+void hip_proj_get_timing(hip_proj_ctx_t* c, double* total_ms, long long* launches) {
+    if (!c) return;
+    hipStreamSynchronize(c->stream);
+    flush_timing(c);
+    for (int k = 0; k < HIP_KT_COUNT; k++) {
+        if (total_ms) total_ms[k] = c->kt_ms[k];
+        if (launches) launches[k] = c->kt_n[k];
+    }
+}
+
+static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
+                                     const ns_solver_params_t* prm, ns_solver_stats_t* stats,
+                                     int iter) {
+    if (!c) return CFD_ERROR_INVALID;
+    cfd_status_t s = validate_params(c, g, prm);
+    if (s != CFD_SUCCESS) return s;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t nx = c->nx, ny = c->ny, nz = c->nz;
+    const double dx = g->dx[0], dy = g->dy[0];
+    const double dz = (nz > 1 && g->dz) ? g->dz[0] : 0.0;
+    const double dt = prm->dt;
+    const bool buoy = (prm->beta != 0.0);
+    if (buoy && !c->have_T) {
+        set_err(CFD_ERROR_INVALID, "projection_hip: Boussinesq buoyancy needs the T field");
+        return CFD_ERROR_INVALID;
+    }
+
+    // source-term tables: compute_source_terms at iter = 0 (solver_explicit_euler.c:317-333)
+    c->h_src_u.resize(ny);
+    c->h_src_v.resize(nx);
+    for (size_t j = 0; j < ny; j++)
+        c->h_src_u[j] = prm->source_amplitude_u * sin(M_PI * g->y[j]) *
+                        exp(-prm->source_decay_rate * iter * dt);
+    for (size_t i = 0; i < nx; i++)
+        c->h_src_v[i] = prm->source_amplitude_v * sin(2.0 * M_PI * g->x[i]) *
+                        exp(-prm->source_decay_rate * iter * dt);
+    HIP_TRY(hipMemcpyAsync(c->src_u_row, c->h_src_u.data(), ny * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->src_v_col, c->h_src_v.data(), nx * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+
+    PredCoef pc;
+    pc.two_dx = 2.0 * dx;
+    pc.two_dy = 2.0 * dy;
+    pc.inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * dz) : 0.0;
+    pc.dx_sq = dx * dx;
+    pc.dy_sq = dy * dy;
+    pc.inv_dz2 = (nz > 1 && g->dz) ? 1.0 / (dz * dz) : 0.0;
+    pc.dt = dt;
+    pc.nu = prm->mu;
+    pc.beta = prm->beta;
+    pc.T_ref = prm->T_ref;
+    pc.g0 = prm->gravity[0];
+    pc.g1 = prm->gravity[1];
+    pc.g2 = prm->gravity[2];
+    const dim3 cg = cell_grid(c);
+    timed(c, HIP_KT_PREDICTOR, [&] {
+        if (buoy)
+            hipLaunchKernelGGL(k_predictor<true>, cg, dim3(256), 0, c->stream, c->geo, pc, c->u,
+                               c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
+        else
+            hipLaunchKernelGGL(k_predictor<false>, cg, dim3(256), 0, c->stream, c->geo, pc, c->u,
+                               c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
+    });
+    HIP_TRY(hipGetLastError());
+
+    // p_new = p (solver_projection.c:108)
+    HIP_TRY(hipMemcpyAsync(c->pn, c->p, field_elems(c) * sizeof(double), hipMemcpyDeviceToDevice,
+                           c->stream));
+
+    double rho = c->rho0;
+    if (rho < 1e-10) rho = 1.0;
+    DivCoef dc;
+    dc.two_dx = 2.0 * dx;
+    dc.two_dy = 2.0 * dy;
+    dc.inv_2dz = pc.inv_2dz;
+    dc.rho_over_dt = rho / dt;
+
+    const int method = c->cfg.poisson_method;
+    cfd_status_t ps;
+    if (method == HIP_POISSON_CG) {
+        ps = cg_solve(c, dx, dy, dz, dc, RHS_FROM_VELOCITY, c->cfg.poisson_tolerance,
+                      c->cfg.poisson_abs_tolerance, c->cfg.poisson_max_iter,
+                      std::max(1, c->cfg.poisson_check_interval), true);
+    } else {
+        s = ensure_aux(c, true, method == HIP_POISSON_JACOBI);
+        if (s != CFD_SUCCESS) return s;
+        const Lap L = make_lap(dx, dy, dz);
+        const int G = tile_grid(c);
+        hipLaunchKernelGGL((k_cg_setup<true, true, false>), dim3(G), dim3(NT), 0, c->stream,
+                           c->geo, L, dc, c->us, c->vs, c->ws, c->rhs, c->pn, c->r, c->st,
+                           c->partials, c->counter, 0.0, 0.0, 0, 1);
+        if (method == HIP_POISSON_JACOBI)
+            HIP_TRY(hipMemsetAsync(c->xt, 0, field_elems(c) * sizeof(double), c->stream));
+        int maxit = c->cfg.poisson_max_iter;
+        ps = relax_solve(c, method, dx, dy, dz, c->cfg.poisson_tolerance,
+                         c->cfg.poisson_abs_tolerance, maxit,
+                         std::max(1, c->cfg.poisson_check_interval), c->cfg.sor_omega);
+    }
+    if (ps != CFD_SUCCESS) {
+        if (ps == CFD_ERROR_MAX_ITER) set_err(CFD_ERROR_MAX_ITER, "projection_hip: pressure solve did not converge");
+        return ps;
+    }
+
+    CorrCoef cc;
+    cc.two_dx = 2.0 * dx;
+    cc.two_dy = 2.0 * dy;
+    cc.inv_2dz = pc.inv_2dz;
+    cc.dt_over_rho = dt / rho;
+    hipLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->red);
+    timed(c, HIP_KT_CORRECTOR, [&] {
+        hipLaunchKernelGGL(k_corrector, cg, dim3(256), 0, c->stream, c->geo, cc, c->us, c->vs,
+                           c->ws, c->pn, c->u, c->v, c->w, c->red);
+    });
+    std::swap(c->p, c->pn);  // memcpy(field->p, p_new) (solver_projection.c:253)
+    HIP_TRY(hipMemcpyAsync(c->h_red, c->red, 8 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    flush_timing(c);
+    if (c->h_red[2]) {
+        set_err(CFD_ERROR_DIVERGED, "projection_hip: NaN/Inf in the flow field");
+        return CFD_ERROR_DIVERGED;
+    }
+    if (stats) {
+        stats->iterations = 1;
+        stats->max_velocity = ord_dec(c->h_red[0]);
+        stats->max_pressure = ord_dec(c->h_red[1]);
+        stats->max_temperature = c->have_T ? c->max_T : 0.0;
+    }
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_step_device(hip_proj_ctx_t* c, const grid* g,
+                                  const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
+    return step_device_impl(c, g, prm, stats, 0);
+}
+
+}  // extern "C"
+
+// Host-buffer path shared by hip_proj_step (one step) and the plugin's solve
+// (n steps, source-term iteration index 0..n-1 as in solver_projection.c:112).
+extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter_internal(
+    hip_proj_ctx_t* c, flow_field* f, const grid* g, const ns_solver_params_t* prm,
+    ns_solver_stats_t* stats, int n_steps) {
+    if (!c || !f || !g || !prm) return CFD_ERROR_INVALID;
+    if (f->nx < 3 || f->ny < 3 || (f->nz > 1 && f->nz < 3)) return CFD_ERROR_INVALID;
+    cfd_status_t s = validate_params(c, g, prm);
+    if (s != CFD_SUCCESS) return s;
+    if (n_steps <= 0) return CFD_SUCCESS;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_V, f->v)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_W, f->w)) != CFD_SUCCESS) return s;
+    if ((s = hip_proj_set_field(c, HIP_FIELD_P, f->p)) != CFD_SUCCESS) return s;
+    const bool need_T = (prm->beta != 0.0) || (prm->alpha > 0.0);
+    if (need_T && f->T) {
+        if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
+    }
+    c->rho0 = f->rho ? f->rho[0] : 1.0;
+    for (int it = 0; it < n_steps; ++it) {
+        s = step_device_impl(c, g, prm, stats, it);
+        if (s != CFD_SUCCESS) break;
+    }
+    if (s == CFD_SUCCESS || s == CFD_ERROR_DIVERGED) {
+        cfd_status_t d = hip_proj_download(c, f);
+        if (d != CFD_SUCCESS) return d;
+    }
+    if (s == CFD_SUCCESS && stats && f->T) {
+        // compute_max_temperature (solver_registry.c:52-62) on the host copy
+        size_t n = c->nx * c->ny * c->nz;
+        double m = f->T[0];
+        for (size_t i = 1; i < n; i++)
+            if (f->T[i] > m) m = f->T[i];
+        stats->max_temperature = m;
+    }
+    return s;
+}
+
+extern "C" __attribute__((visibility("hidden"))) int hip_proj_matches_internal(const hip_proj_ctx_t* c,
+                                                                    size_t nx, size_t ny,
+                                                                    size_t nz) {
+    return c && c->nx == nx && c->ny == ny && c->nz == nz;
+}
+
+extern "C" {
+
+cfd_status_t hip_proj_step(hip_proj_ctx_t* c, flow_field* f, const grid* g,
+                           const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
+    return hip_proj_step_iter_internal(c, f, g, prm, stats, 1);
+}
+
+cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* c, int method, double* x, const double* rhs,
+                                    double dx, double dy, double dz,
+                                    const poisson_solver_params_t* params,
+                                    poisson_solver_stats_t* stats) {
+    if (!c || !x || !rhs) return CFD_ERROR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    double rel = 1e-6, abs_tol = 1e-10, omega = 0.0;
+    int maxit = (method == HIP_POISSON_JACOBI) ? 2000 : 5000, ci = 1;
+    if (params) {
+        rel = params->tolerance;
+        abs_tol = params->absolute_tolerance;
+        maxit = params->max_iterations;
+        ci = std::max(1, params->check_interval);
+        omega = params->omega;
+        if (params->preconditioner != POISSON_PRECOND_NONE) {
+            set_err(CFD_ERROR_UNSUPPORTED, "hip_proj_poisson_solve: preconditioner not supported");
+            return CFD_ERROR_UNSUPPORTED;
+        }
+    }
+    cfd_status_t s = ensure_aux(c, true, method == HIP_POISSON_JACOBI);
+    if (s != CFD_SUCCESS) return s;
+    HIP_TRY(hipMemcpy2DAsync(c->rhs, c->px * sizeof(double), rhs, c->nx * sizeof(double),
+                             c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
+                             c->stream));
+    HIP_TRY(hipMemcpy2DAsync(c->pn, c->px * sizeof(double), x, c->nx * sizeof(double),
+                             c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
+                             c->stream));
+    if (method == HIP_POISSON_JACOBI)
+        HIP_TRY(hipMemcpyAsync(c->xt, c->pn, field_elems(c) * sizeof(double),
+                               hipMemcpyDeviceToDevice, c->stream));
+    if (method == HIP_POISSON_CG) {
+        DivCoef dc{};
+        s = cg_solve(c, dx, dy, dz, dc, RHS_FROM_ARRAY, rel, abs_tol, maxit, ci, true);
+    } else {
+        s = relax_solve(c, method, dx, dy, dz, rel, abs_tol, maxit, ci, omega);
+    }
+    HIP_TRY(hipMemcpy2DAsync(x, c->nx * sizeof(double), c->pn, c->px * sizeof(double),
+                             c->nx * sizeof(double), c->ny * c->nz, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (stats) {
+        *stats = c->pstats;
+        stats->elapsed_time_ms = 0.0;
+    }
+    return s;
+}
+
+double hip_proj_cg_fixed_iters(hip_proj_ctx_t* c, const double* rhs_host, double dx, double dy,
+                               double dz, int iters) {
+    if (!c || !rhs_host || iters <= 0) return -1.0;
+    if (hipSetDevice(c->device) != hipSuccess) return -1.0;
+    if (ensure_aux(c, true, false) != CFD_SUCCESS) return -1.0;
+    if (hipMemcpy2DAsync(c->rhs, c->px * sizeof(double), rhs_host, c->nx * sizeof(double),
+                         c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
+                         c->stream) != hipSuccess)
+        return -1.0;
+    hipMemsetAsync(c->pn, 0, field_elems(c) * sizeof(double), c->stream);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    DivCoef dc{};
+    hipEventRecord(a, c->stream);
+    // zero tolerances: no early exit, exactly `iters` iterations
+    cfd_status_t s = cg_solve(c, dx, dy, dz, dc, RHS_FROM_ARRAY, 0.0, 0.0, iters, 1, false);
+    (void)s;
+    hipEventRecord(b, c->stream);
+    hipEventSynchronize(b);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return (double)ms;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+/*
+ * cfd_host.h -- standalone host-side mirror of the reference's public API
+ * around the projection hot path (libcfd_host.so).
+ *
+ * When the HIP projection is dropped into a reference build, the reference
+ * provides all of these symbols itself and only libcfd_hip.so is linked. For
+ * standalone use (our tests, bench.py, examples) libcfd_host.so provides the
+ * same functions with the same signatures and semantics:
+ *   errors       lib/include/cfd/core/cfd_status.h:29-46, lib/src/core/logging.c:13-90
+ *   grid         lib/include/cfd/core/grid.h:56-88, lib/src/core/grid.c:9-127
+ *   flow field   lib/include/cfd/solvers/navier_stokes_solver.h:410-432
+ *   BCs (3-D)    lib/include/cfd/boundary/boundary_conditions.h:1222-1255
+ *   registry     lib/include/cfd/solvers/navier_stokes_solver.h:291-371,
+ *                lib/src/api/solver_registry.c:202-494
+ *   simulation   lib/include/cfd/api/simulation_api.h (init_simulation_with_solver,
+ *                run_simulation_step, run_simulation_solve, free_simulation)
+ * cfd_registry_register_defaults registers the HIP projection solvers when
+ * libcfd_hip.so is loaded in the process (it looks up cfd_hip_register_solvers).
+ */
+#ifndef CFD_HIP_CFD_HOST_H
+#define CFD_HIP_CFD_HOST_H
+
+#include "cfd_hip/cfd_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* errors */
+CFD_HIP_EXPORT void cfd_set_error(cfd_status_t status, const char* message);
+CFD_HIP_EXPORT const char* cfd_get_last_error(void);
+CFD_HIP_EXPORT cfd_status_t cfd_get_last_status(void);
+CFD_HIP_EXPORT const char* cfd_get_error_string(cfd_status_t status);
+CFD_HIP_EXPORT void cfd_clear_error(void);
+
+/* grid */
+CFD_HIP_EXPORT grid* grid_create(size_t nx, size_t ny, size_t nz, double xmin, double xmax,
+                                 double ymin, double ymax, double zmin, double zmax);
+CFD_HIP_EXPORT void grid_destroy(grid* grid);
+CFD_HIP_EXPORT void grid_initialize_uniform(grid* grid);
+
+/* flow field */
+CFD_HIP_EXPORT flow_field* flow_field_create(size_t nx, size_t ny, size_t nz);
+CFD_HIP_EXPORT void flow_field_destroy(flow_field* field);
+CFD_HIP_EXPORT void initialize_flow_field(flow_field* field, const grid* grid);
+CFD_HIP_EXPORT ns_solver_params_t ns_solver_params_default(void);
+CFD_HIP_EXPORT ns_solver_stats_t ns_solver_stats_default(void);
+
+/* boundary conditions on host arrays */
+CFD_HIP_EXPORT cfd_status_t bc_apply_scalar_3d(double* field, size_t nx, size_t ny, size_t nz,
+                                               size_t stride_z, bc_type_t type);
+CFD_HIP_EXPORT cfd_status_t bc_apply_velocity_3d(double* u, double* v, double* w, size_t nx,
+                                                 size_t ny, size_t nz, size_t stride_z,
+                                                 bc_type_t type);
+CFD_HIP_EXPORT cfd_status_t bc_apply_dirichlet_scalar_3d(double* field, size_t nx, size_t ny,
+                                                         size_t nz, size_t stride_z,
+                                                         const bc_dirichlet_values_t* values);
+CFD_HIP_EXPORT cfd_status_t bc_apply_dirichlet_velocity_3d(
+    double* u, double* v, double* w, size_t nx, size_t ny, size_t nz, size_t stride_z,
+    const bc_dirichlet_values_t* u_values, const bc_dirichlet_values_t* v_values,
+    const bc_dirichlet_values_t* w_values);
+
+/* registry and solver lifecycle */
+CFD_HIP_EXPORT ns_solver_registry_t* cfd_registry_create(void);
+CFD_HIP_EXPORT void cfd_registry_destroy(ns_solver_registry_t* registry);
+CFD_HIP_EXPORT void cfd_registry_register_defaults(ns_solver_registry_t* registry);
+CFD_HIP_EXPORT int cfd_registry_register(ns_solver_registry_t* registry, const char* type_name,
+                                         ns_solver_factory_func factory);
+CFD_HIP_EXPORT int cfd_registry_unregister(ns_solver_registry_t* registry, const char* type_name);
+CFD_HIP_EXPORT int cfd_registry_list(ns_solver_registry_t* registry, const char** names,
+                                     int max_count);
+CFD_HIP_EXPORT int cfd_registry_has(ns_solver_registry_t* registry, const char* type_name);
+CFD_HIP_EXPORT const char* cfd_registry_get_description(ns_solver_registry_t* registry,
+                                                        const char* type_name);
+CFD_HIP_EXPORT ns_solver_t* cfd_solver_create(ns_solver_registry_t* registry,
+                                              const char* type_name);
+CFD_HIP_EXPORT void solver_destroy(ns_solver_t* solver);
+CFD_HIP_EXPORT cfd_status_t solver_init(ns_solver_t* solver, const grid* grid,
+                                        const ns_solver_params_t* params);
+CFD_HIP_EXPORT cfd_status_t solver_step(ns_solver_t* solver, flow_field* field, const grid* grid,
+                                        const ns_solver_params_t* params,
+                                        ns_solver_stats_t* stats);
+CFD_HIP_EXPORT cfd_status_t solver_solve(ns_solver_t* solver, flow_field* field,
+                                         const grid* grid, const ns_solver_params_t* params,
+                                         ns_solver_stats_t* stats);
+CFD_HIP_EXPORT int cfd_backend_is_available(ns_solver_backend_t backend);
+CFD_HIP_EXPORT const char* cfd_backend_get_name(ns_solver_backend_t backend);
+
+/* simulation API subset (simulation_api.h) */
+typedef struct {
+    grid* grid;
+    flow_field* field;
+    ns_solver_params_t params;
+    ns_solver_t* solver;
+    ns_solver_registry_t* registry;
+    ns_solver_stats_t last_stats;
+    void* outputs;          /* output registry: not provided by this mirror (NULL) */
+    char* run_prefix;
+    double current_time;
+    char output_base_dir[512];
+} simulation_data;
+
+CFD_HIP_EXPORT simulation_data* init_simulation_with_solver(size_t nx, size_t ny, size_t nz,
+                                                            double xmin, double xmax,
+                                                            double ymin, double ymax,
+                                                            double zmin, double zmax,
+                                                            const char* solver_type);
+CFD_HIP_EXPORT void free_simulation(simulation_data* sim);
+CFD_HIP_EXPORT cfd_status_t run_simulation_step(simulation_data* sim);
+CFD_HIP_EXPORT cfd_status_t run_simulation_solve(simulation_data* sim);
+CFD_HIP_EXPORT const ns_solver_stats_t* simulation_get_stats(const simulation_data* sim);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CFD_HIP_CFD_HOST_H */

@@ -1,0 +1,171 @@
+/*
+ * projection_hip.h -- C-ABI of the MI355X-native Chorin projection step.
+ *
+ * This is the drop-in boundary. Two layers:
+ *
+ *  1. The plugin factory `create_projection_hip_solver` returns an ns_solver_t
+ *     (cfd_abi.h) whose step/solve have exactly the semantics of the
+ *     reference's scalar `projection` solver (solver_registry.c:921-972 ->
+ *     solver_projection.c:46-297), so a reference build registers it with
+ *        cfd_registry_register(registry, "projection_hip", create_projection_hip_solver);
+ *     next to `projection_gpu` (solver_registry.c:233-240) and drives it
+ *     unchanged through init_simulation* / run_simulation_step / solver_step.
+ *     `projection_hip_rbsor` and `projection_hip_jacobi` select the Red-Black
+ *     SOR / Jacobi pressure solver instead of CG (the reference hard-codes CG
+ *     in the projection, solver_projection.c:217-218).
+ *
+ *  2. The thin context API (`hip_proj_*`) the plugin calls. It owns all
+ *     device memory, so it also serves device-resident drivers (bench.py,
+ *     long runs): upload once, step many times in HBM, download at the end.
+ *     It replaces the reference's per-call CUDA driver
+ *     solve_projection_method_gpu (lib/src/solvers/gpu/solver_projection_gpu.cu:617-770)
+ *     and the persistent-context API of lib/include/cfd/core/gpu_device.h:145-194.
+ *
+ * No HIP or torch types appear in any signature.
+ */
+#ifndef CFD_HIP_PROJECTION_HIP_H
+#define CFD_HIP_PROJECTION_HIP_H
+
+#include "cfd_hip/cfd_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NS_SOLVER_TYPE_PROJECTION_HIP        "projection_hip"
+#define NS_SOLVER_TYPE_PROJECTION_HIP_RBSOR  "projection_hip_rbsor"
+#define NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI "projection_hip_jacobi"
+
+/* Pressure-Poisson method used inside the HIP projection step. */
+typedef enum {
+    HIP_POISSON_CG = 0,       /* textbook CG, linear_solver_cg.c:290-461 */
+    HIP_POISSON_REDBLACK = 1, /* Red-Black SOR, linear_solver_redblack.c:80-147 */
+    HIP_POISSON_JACOBI = 2    /* Jacobi, linear_solver_jacobi.c:76-129 */
+} hip_poisson_method_t;
+
+/* Device/solver configuration (role of gpu_config_t, gpu_device.h:32-53). The
+ * Poisson defaults are the CPU reference's (linear_solver.c:37-47), not the
+ * reference GPU's looser 1e-3 / 1000 (solver_projection_gpu.cu:301-302). */
+typedef struct {
+    int device;                   /* HIP device ordinal; -1 = current device */
+    int poisson_method;           /* hip_poisson_method_t */
+    double poisson_tolerance;     /* relative residual tolerance (1e-6) */
+    double poisson_abs_tolerance; /* absolute residual tolerance (1e-10) */
+    int poisson_max_iter;         /* 5000 for CG/RB-SOR, 2000 for Jacobi */
+    int poisson_check_interval;   /* convergence check period (1) */
+    double sor_omega;             /* <= 0: optimal omega (linear_solver_internal.h:184-220) */
+    int poll_interval;            /* iterations launched between host convergence polls */
+    int kchunk;                   /* z planes per stencil tile; 0 = auto */
+    int verbose;
+} hip_proj_config_t;
+
+typedef struct hip_proj_ctx hip_proj_ctx_t;
+
+/* Which device array a helper addresses. */
+typedef enum {
+    HIP_FIELD_U = 0,
+    HIP_FIELD_V = 1,
+    HIP_FIELD_W = 2,
+    HIP_FIELD_P = 3,
+    HIP_FIELD_T = 4
+} hip_field_id_t;
+
+/* Per-kernel timing (filled when profiling is enabled). */
+typedef enum {
+    HIP_KT_PREDICTOR = 0,
+    HIP_KT_CG_SETUP = 1,
+    HIP_KT_CG_SWEEP_A = 2, /* p = r + beta p, Ap on the fly, (p,Ap), deferred x += alpha p */
+    HIP_KT_CG_SWEEP_B = 3, /* r -= alpha A p (Ap recomputed), (r,r) */
+    HIP_KT_CORRECTOR = 4,
+    HIP_KT_RELAX = 5,      /* one RB-SOR colour pass or one Jacobi sweep */
+    HIP_KT_RESIDUAL = 6,   /* L-infinity residual for the relaxation methods */
+    HIP_KT_COUNT = 7
+} hip_kernel_timer_t;
+
+CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);
+
+/* 1 if a HIP device is usable, else 0 (role of gpu_is_available). */
+CFD_HIP_EXPORT int hip_projection_available(void);
+
+/* Create a context for an nx*ny*nz grid (nz == 1: 2D). Returns NULL and sets
+ * the thread-local error on failure. */
+CFD_HIP_EXPORT hip_proj_ctx_t* hip_proj_create(size_t nx, size_t ny, size_t nz,
+                                               const hip_proj_config_t* cfg);
+CFD_HIP_EXPORT void hip_proj_destroy(hip_proj_ctx_t* ctx);
+
+/* One projection step on caller-owned host buffers: upload u,v,w,p (and T),
+ * run the step in HBM, download. Same contract as the reference `projection`
+ * step: status codes, preserved caller boundary faces, stats. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_step(hip_proj_ctx_t* ctx, flow_field* field, const grid* g,
+                                          const ns_solver_params_t* params,
+                                          ns_solver_stats_t* stats);
+
+/* Device-resident path. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_upload(hip_proj_ctx_t* ctx, const flow_field* field);
+CFD_HIP_EXPORT cfd_status_t hip_proj_download(hip_proj_ctx_t* ctx, flow_field* field);
+CFD_HIP_EXPORT cfd_status_t hip_proj_step_device(hip_proj_ctx_t* ctx, const grid* g,
+                                                 const ns_solver_params_t* params,
+                                                 ns_solver_stats_t* stats);
+/* Copy one device field (unpadded, nx*ny*nz doubles) to / from host memory. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_get_field(hip_proj_ctx_t* ctx, int field_id, double* host);
+CFD_HIP_EXPORT cfd_status_t hip_proj_set_field(hip_proj_ctx_t* ctx, int field_id,
+                                               const double* host);
+/* Fill a device field with a constant. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* ctx, int field_id, double value);
+/* Density used by the step (the reference reads field->rho[0] only). */
+CFD_HIP_EXPORT cfd_status_t hip_proj_set_density(hip_proj_ctx_t* ctx, double rho0);
+
+/* Caller-side boundary conditions applied on the device between steps (what
+ * the reference drivers do on the host with bc_apply_scalar_3d /
+ * bc_apply_dirichlet_velocity_3d, boundary_conditions.h:1222-1255). */
+CFD_HIP_EXPORT cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* ctx, int field_id,
+                                                     bc_type_t type);
+CFD_HIP_EXPORT cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* ctx, int field_id,
+                                                     const bc_dirichlet_values_t* values);
+
+/* Pressure-solver statistics of the most recent step. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_get_poisson_stats(hip_proj_ctx_t* ctx,
+                                                       poisson_solver_stats_t* stats);
+
+/* Kernel timing with HIP events on the context's stream. */
+CFD_HIP_EXPORT void hip_proj_enable_timing(hip_proj_ctx_t* ctx, int enable);
+CFD_HIP_EXPORT void hip_proj_reset_timing(hip_proj_ctx_t* ctx);
+/* total_ms[k] and launches[k] for each hip_kernel_timer_t k. */
+CFD_HIP_EXPORT void hip_proj_get_timing(hip_proj_ctx_t* ctx, double* total_ms, long long* launches);
+
+CFD_HIP_EXPORT cfd_status_t hip_proj_synchronize(hip_proj_ctx_t* ctx);
+/* Bytes of device memory held by the context. */
+CFD_HIP_EXPORT size_t hip_proj_device_bytes(const hip_proj_ctx_t* ctx);
+/* Row pitch (in doubles) of the padded device layout. */
+CFD_HIP_EXPORT size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx);
+
+/* Standalone fixed-iteration CG microbenchmark on the context's buffers:
+ * solves lap(x) = rhs (rhs given on host, x0 = 0) for exactly `iters`
+ * iterations with no early exit. Returns elapsed device ms (events). */
+CFD_HIP_EXPORT double hip_proj_cg_fixed_iters(hip_proj_ctx_t* ctx, const double* rhs_host,
+                                              double dx, double dy, double dz, int iters);
+
+/* Standalone pressure-Poisson solve on host buffers, the HIP counterpart of
+ * poisson_solver_solve with a POISSON_BACKEND_GPU solver (linear_solver.c:487-509,
+ * poisson_solver_cg_gpu.cu:135-178): upload x and rhs, solve lap(x) = rhs with
+ * the method given (CG / RB-SOR / Jacobi; Neumann BCs as the reference's default
+ * apply_bc), download x. params == NULL uses poisson_solver_params_default()
+ * (Jacobi: max_iterations 2000, linear_solver.c:274-276). */
+CFD_HIP_EXPORT cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* ctx, int method, double* x,
+                                                   const double* rhs, double dx, double dy,
+                                                   double dz,
+                                                   const poisson_solver_params_t* params,
+                                                   poisson_solver_stats_t* stats);
+
+/* ---- plugin surface ------------------------------------------------------ */
+CFD_HIP_EXPORT ns_solver_t* create_projection_hip_solver(void);
+CFD_HIP_EXPORT ns_solver_t* create_projection_hip_rbsor_solver(void);
+CFD_HIP_EXPORT ns_solver_t* create_projection_hip_jacobi_solver(void);
+/* Registers the three names above through cfd_registry_register(). */
+CFD_HIP_EXPORT void cfd_hip_register_solvers(ns_solver_registry_t* registry);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CFD_HIP_PROJECTION_HIP_H */

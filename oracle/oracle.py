@@ -1,0 +1,154 @@
+"""TEST INFRASTRUCTURE ONLY -- Python handle on the CPU oracle (liboracle.so).
+
+The oracle is a plain-C restatement of the reference's scalar/OpenMP
+projection path (see oracle.h for the pinning statement). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may use it, and only
+as the checker or the timed CPU baseline -- never as the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from cfd_amd import _abi as A
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB = ORACLE_DIR / "build" / "liboracle.so"
+_lib = None
+
+
+def build(force: bool = False) -> Path:
+    if force and LIB.exists():
+        LIB.unlink()
+    subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, stdout=subprocess.DEVNULL)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = C.CDLL(str(LIB))
+        P = C.POINTER
+        d = A.c_double_p
+        sz = C.c_size_t
+
+        def sig(name, res, *args):
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = list(args)
+
+        sig("oracle_set_threads", None, C.c_int)
+        sig("oracle_get_threads", C.c_int)
+        sig("oracle_set_poisson_cap", None, C.c_int)
+        sig("oracle_projection_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
+            P(A.SolverStats), C.c_int, P(C.c_int))
+        sig("oracle_last_phase_ms", None, d)
+        sig("oracle_cg_solve", C.c_int, d, d, sz, sz, sz, C.c_double, C.c_double, C.c_double,
+            P(A.PoissonParams), P(A.PoissonStats))
+        sig("oracle_redblack_solve", C.c_int, d, d, sz, sz, sz, C.c_double, C.c_double,
+            C.c_double, P(A.PoissonParams), P(A.PoissonStats))
+        sig("oracle_jacobi_solve", C.c_int, d, d, d, sz, sz, sz, C.c_double, C.c_double,
+            C.c_double, P(A.PoissonParams), P(A.PoissonStats))
+        sig("oracle_poisson_params_default", A.PoissonParams)
+        sig("oracle_cg_fixed_iters", C.c_double, d, d, sz, sz, sz, C.c_double, C.c_double,
+            C.c_double, C.c_int)
+        sig("oracle_bc_neumann_3d", None, d, sz, sz, sz)
+        sig("oracle_bc_periodic_3d", None, d, sz, sz, sz)
+        sig("oracle_bc_dirichlet_3d", None, d, sz, sz, sz, P(A.DirichletValues))
+        sig("oracle_poisson_apply_bc", None, d, sz, sz, sz)
+        sig("oracle_grid_create_uniform", P(A.Grid), sz, sz, sz, C.c_double, C.c_double,
+            C.c_double, C.c_double, C.c_double, C.c_double)
+        sig("oracle_grid_destroy", None, P(A.Grid))
+        sig("oracle_field_create", P(A.FlowField), sz, sz, sz)
+        sig("oracle_field_destroy", None, P(A.FlowField))
+        sig("oracle_params_default", A.SolverParams)
+        sig("oracle_max_velocity_pressure", None, P(A.FlowField), d, d)
+        _lib = L
+    return _lib
+
+
+def _dp(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(A.c_double_p)
+
+
+def set_threads(n: int) -> None:
+    lib().oracle_set_threads(n)
+
+
+def projection_step(field, grid, params, poisson=A.ORACLE_POISSON_CG):
+    """One reference `projection` step on a cfd_amd.api.FlowField / Grid.
+    Returns (status, stats, poisson_iterations)."""
+    st = A.SolverStats()
+    it = C.c_int(0)
+    s = lib().oracle_projection_step(field.ptr, grid.ptr, C.byref(params), C.byref(st),
+                                     poisson, C.byref(it))
+    return s, st, it.value
+
+
+def last_phase_ms():
+    out = (C.c_double * 4)()
+    lib().oracle_last_phase_ms(out)
+    return list(out)
+
+
+def poisson_params(**kw) -> A.PoissonParams:
+    p = lib().oracle_poisson_params_default()
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def cg_solve(x: np.ndarray, rhs: np.ndarray, dx, dy, dz, params=None):
+    nz, ny, nx = x.shape
+    st = A.PoissonStats()
+    s = lib().oracle_cg_solve(_dp(x), _dp(rhs), nx, ny, nz, dx, dy, dz,
+                              C.byref(params) if params is not None else None, C.byref(st))
+    return s, st
+
+
+def redblack_solve(x, rhs, dx, dy, dz, params=None):
+    nz, ny, nx = x.shape
+    st = A.PoissonStats()
+    s = lib().oracle_redblack_solve(_dp(x), _dp(rhs), nx, ny, nz, dx, dy, dz,
+                                    C.byref(params) if params is not None else None, C.byref(st))
+    return s, st
+
+
+def jacobi_solve(x, rhs, dx, dy, dz, params=None):
+    nz, ny, nx = x.shape
+    st = A.PoissonStats()
+    xt = x.copy()
+    s = lib().oracle_jacobi_solve(_dp(x), _dp(xt), _dp(rhs), nx, ny, nz, dx, dy, dz,
+                                  C.byref(params) if params is not None else None, C.byref(st))
+    return s, st
+
+
+def cg_fixed_iters(x, rhs, dx, dy, dz, iters) -> float:
+    nz, ny, nx = x.shape
+    return lib().oracle_cg_fixed_iters(_dp(x), _dp(rhs), nx, ny, nz, dx, dy, dz, iters)
+
+
+def bc_neumann(a: np.ndarray):
+    nz, ny, nx = a.shape
+    lib().oracle_bc_neumann_3d(_dp(a), nx, ny, nz)
+
+
+def bc_periodic(a: np.ndarray):
+    nz, ny, nx = a.shape
+    lib().oracle_bc_periodic_3d(_dp(a), nx, ny, nz)
+
+
+def bc_dirichlet(a: np.ndarray, values: A.DirichletValues):
+    nz, ny, nx = a.shape
+    lib().oracle_bc_dirichlet_3d(_dp(a), nx, ny, nz, C.byref(values))
+
+
+def poisson_apply_bc(a: np.ndarray):
+    nz, ny, nx = a.shape
+    lib().oracle_poisson_apply_bc(_dp(a), nx, ny, nz)
