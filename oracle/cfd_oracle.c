@@ -29,10 +29,16 @@
 
 static int g_threads = 1;
 static int g_poisson_cap = 0; /* >0: timing-only sample, CG capped and accepted */
+static int g_have_pparams = 0;
+static poisson_solver_params_t g_pparams;
 static double g_phase_ms[4];
 
 void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 void oracle_set_poisson_cap(int n) { g_poisson_cap = n < 0 ? 0 : n; }
+void oracle_set_projection_poisson_params(const poisson_solver_params_t* p) {
+    g_have_pparams = p != NULL;
+    if (p) g_pparams = *p;
+}
 int oracle_get_threads(void) { return g_threads; }
 void oracle_last_phase_ms(double out[4]) { memcpy(out, g_phase_ms, sizeof(g_phase_ms)); }
 
@@ -923,7 +929,7 @@ cfd_status_t oracle_projection_step(flow_field* field, const grid* grid,
     cfd_status_t ps;
     poisson_solver_params_t capped = oracle_poisson_params_default();
     capped.max_iterations = g_poisson_cap;
-    const poisson_solver_params_t* pp = g_poisson_cap > 0 ? &capped : NULL;
+    const poisson_solver_params_t* pp = g_poisson_cap > 0 ? &capped : (g_have_pparams ? &g_pparams : NULL);
     if (pkind == ORACLE_POISSON_REDBLACK)
         ps = oracle_redblack_solve(pn, rhs, nx, ny, nz, dx, dy, dz, pp, &pst);
     else if (pkind == ORACLE_POISSON_JACOBI)

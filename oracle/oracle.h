@@ -32,6 +32,10 @@ void oracle_set_threads(int nthreads);
  * pressure solve at n iterations and accepts the result (0 = off). */
 void oracle_set_poisson_cap(int n);
 int oracle_get_threads(void);
+/* Override the pressure-solver parameters used inside oracle_projection_step
+ * (the reference always passes NULL = defaults, linear_solver.c:684); NULL
+ * restores the defaults. Used to pair with a HIP context configured alike. */
+void oracle_set_projection_poisson_params(const poisson_solver_params_t* p);
 
 /* grid.c:9-127 (grid_create + grid_initialize_uniform) */
 grid* oracle_grid_create_uniform(size_t nx, size_t ny, size_t nz, double xmin, double xmax,

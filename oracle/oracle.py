@@ -45,6 +45,7 @@ def lib():
         sig("oracle_set_threads", None, C.c_int)
         sig("oracle_get_threads", C.c_int)
         sig("oracle_set_poisson_cap", None, C.c_int)
+        sig("oracle_set_projection_poisson_params", None, P(A.PoissonParams))
         sig("oracle_projection_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
             P(A.SolverStats), C.c_int, P(C.c_int))
         sig("oracle_last_phase_ms", None, d)
@@ -89,6 +90,10 @@ def projection_step(field, grid, params, poisson=A.ORACLE_POISSON_CG):
     s = lib().oracle_projection_step(field.ptr, grid.ptr, C.byref(params), C.byref(st),
                                      poisson, C.byref(it))
     return s, st, it.value
+
+
+def set_projection_poisson_params(params=None):
+    lib().oracle_set_projection_poisson_params(C.byref(params) if params is not None else None)
 
 
 def last_phase_ms():
