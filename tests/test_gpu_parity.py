@@ -234,12 +234,22 @@ def test_max_iter_failure_leaves_field(hip_lib):
     ctx.close()
 
 
-def test_nan_reports_diverged(hip_lib):
+@pytest.mark.parametrize("where", [(0, 0, 0), (3, 4, 5)])
+def test_nonfinite_input_status_matches_oracle(hip_lib, where):
+    """A NaN on the boundary survives the step -> CFD_ERROR_DIVERGED
+    (solver_projection.c:281-289); an interior NaN is absorbed by the +-100
+    velocity clamp (fmin(100, NaN) = 100, :180-182) exactly as in the reference."""
     g, f, p = cases.tg3(17)
-    f.u[3, 4, 5] = float("nan")
+    f.u[where] = float("nan")
+    fo = _clone(g, f)
     ctx = api.HipProjection(17, 17, 17)
     s = ctx.step(f, g, p)
-    assert s in (A.CFD_ERROR_DIVERGED, A.CFD_ERROR_MAX_ITER)
+    so, _, _ = oracle.projection_step(fo, g, p)
+    assert s == so
+    assert s == (A.CFD_ERROR_DIVERGED if where == (0, 0, 0) else A.CFD_SUCCESS)
+    if s == A.CFD_SUCCESS:
+        for k in ("u", "v", "w", "p"):
+            assert _rel_maxdiff(getattr(f, k), getattr(fo, k)) <= CG_FIELD_RTOL, k
     ctx.close()
 
 

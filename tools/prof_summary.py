@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output: per-kernel call count / average duration
+from the kernel-trace stats, and per-dispatch FETCH_SIZE / WRITE_SIZE (KB)
+averaged per kernel from separate PMC passes.
+
+usage: prof_summary.py <prof_dir> [--cells N]
+  <prof_dir>/trace/run_kernel_stats.csv, <prof_dir>/fetch/run_counter_collection.csv,
+  <prof_dir>/write/run_counter_collection.csv (the PMC files are optional)
+"""
+import csv
+import re
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def short(name: str) -> str:
+    m = re.search(r"(k_\w+(?:<[^>]*>)?)", name)
+    return m.group(1) if m else name.split("(")[0][:60]
+
+
+def stats(path: Path):
+    out = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            out[short(row["Name"])] = (int(row["Calls"]), float(row["AverageNs"]) / 1e3,
+                                       float(row["TotalDurationNs"]) / 1e6)
+    return out
+
+
+def pmc(path: Path):
+    acc = defaultdict(list)
+    if not path.exists():
+        return {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    d = Path(sys.argv[1])
+    cells = None
+    if "--cells" in sys.argv:
+        cells = float(sys.argv[sys.argv.index("--cells") + 1])
+    st = stats(d / "trace" / "run_kernel_stats.csv")
+    fe = pmc(d / "fetch" / "run_counter_collection.csv")
+    wr = pmc(d / "write" / "run_counter_collection.csv")
+    print(f"{'kernel':34s} {'calls':>6s} {'avg_us':>10s} {'total_ms':>10s} "
+          f"{'FETCH_KB':>12s} {'WRITE_KB':>12s}" + ("  B/cell(fetch,write)" if cells else ""))
+    for k, (n, avg, tot) in sorted(st.items(), key=lambda kv: -kv[1][2]):
+        f = fe.get(k)
+        w = wr.get(k)
+        line = f"{k:34s} {n:6d} {avg:10.2f} {tot:10.2f} " \
+               f"{(f'{f:12.0f}' if f is not None else ' ' * 12)} " \
+               f"{(f'{w:12.0f}' if w is not None else ' ' * 12)}"
+        if cells and (f is not None or w is not None):
+            fb = f * 1024 / cells if f is not None else float("nan")
+            wb = w * 1024 / cells if w is not None else float("nan")
+            line += f"  {fb:6.2f},{wb:6.2f}"
+        print(line)
+
+
+if __name__ == "__main__":
+    main()
