@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-cg-iters", type=int, default=10,
                     help="CG iterations timed in the CPU baseline sample")
     ap.add_argument("--kchunk", type=int, default=0)
+    ap.add_argument("--sweep-rows", type=int, default=8)
     return ap.parse_args()
 
 
@@ -77,7 +78,8 @@ def main():
     nu = 1.0 / args.re
     g = api.Grid(n, n, n, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
     params = api.validation_params(args.dt, nu)
-    ctx = api.HipProjection(n, n, n, device=local, kchunk=args.kchunk)
+    ctx = api.HipProjection(n, n, n, device=local, kchunk=args.kchunk,
+                             sweep_rows=args.sweep_rows)
     for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
         ctx.fill(fid, 0.0)
     ctx.set_density(1.0)
@@ -159,7 +161,7 @@ def main():
             "cg_iters_per_step": iters,
             "cg_iter_ms": round(cg_iter_ms, 4),
             "cg_iter_GBps_survey80": round(cg_iter_gbps_survey, 1),
-            "roofline": {"bound": "hbm", "kernel": "k_cg_sweep_a",
+            "roofline": {"bound": "hbm", "kernel": "k_cgA",
                          "achieved": round(ach_a, 1) if ach_a else None,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach_a / HBM_PEAK_GBPS, 4) if ach_a else None,

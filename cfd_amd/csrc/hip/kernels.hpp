@@ -133,6 +133,37 @@ __device__ __forceinline__ bool grid_sum_last(double block_total, double* partia
     return true;
 }
 
+// Same protocol for NTH-thread workgroups; `sh` needs NTH/64 doubles of LDS
+// that no wave still reads (callers pass their stencil row buffer after the
+// workgroup barrier that ends the sweep).
+template <int NTH>
+__device__ __forceinline__ bool grid_sum_last_n(double block_total, double* partials,
+                                                unsigned* counter, double* sh, int* flag,
+                                                double& total) {
+    if (threadIdx.x == 0) {
+        store_sc1(&partials[blockIdx.x], block_total);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        *flag = (t == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (*flag == 0) return false;
+    double s = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += NTH) s += load_sc1(&partials[b]);
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0;
+#pragma unroll
+        for (int w = 0; w < NTH / 64; ++w) a += sh[w];
+        total = a;
+        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
 // Order-preserving encoding of doubles into uint64 for atomicMax.
 __device__ __forceinline__ unsigned long long ord_enc(double d) {
     unsigned long long b = (unsigned long long)__double_as_longlong(d);
@@ -254,56 +285,159 @@ __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
     }
 }
 
-// ---------------------------------------------------------------------------
-// CG sweep A of iteration `it`:
-//   p_it = r_it + beta p_{it-1}          (p_0 = r_0), written to pnew
-//   (p_it, A p_it) with A = -lap, A p computed in registers, never stored
-//   x += alpha_{it-1} p_{it-1}           (the x update of the previous
-//                                         iteration, deferred into this sweep)
-// HBM per interior cell: read r, pold, x; write pnew, x (FIRST: read r, write pnew).
-// ---------------------------------------------------------------------------
-template <bool FIRST>
-__global__ __launch_bounds__(NT) void k_cg_sweep_a(Geo g, Lap L, const double* __restrict__ r,
-                                                   const double* __restrict__ pold,
-                                                   double* __restrict__ pnew,
-                                                   double* __restrict__ x, CgState* st,
-                                                   double* partials, unsigned* counter, int it) {
-    __shared__ double sh[NWAVE];
+// ===========================================================================
+// Production CG sweeps ("row-pair" kernels).
+//
+// Tile = 128 (x) x TY (y) x kc (z); one wavefront per y row, each lane owns
+// the x pair (i0, i0+1) and moves it with 16-B loads/stores (the streaming
+// width MI355X's memory path prefers). x neighbours come from the adjacent
+// lanes (__shfl), y neighbours from the TY+2 rows the workgroup's waves
+// publish in LDS each plane (double-buffered, one barrier per plane), z
+// neighbours from registers. Workgroups are mapped to tiles XCD-aware: the 8
+// XCDs each get a contiguous band of tiles, so the y halo rows a workgroup
+// reads were just streamed into the same XCD's L2 by its neighbour.
+// Measured at 512^3 (tools/mb/stencil_mb6.hip): 5.2 TB/s for sweep A versus
+// 4.3-4.5 TB/s for one-cell-per-lane designs.
+// ===========================================================================
+struct SGeo {
+    int nx, ny, nz;
+    long long px, ps, sz;
+    int k0, k1, kc;
+    int tiles_x, tiles_y, tiles_z;  // tiles of 128 x TY x kc
+};
+
+__device__ __forceinline__ int xcd_tile(int b, int nt) {
+    // bijective remap: block b runs on XCD b % 8 (round-robin dispatch);
+    // give each XCD a contiguous range of tiles (speed only, never correctness)
+    const int q = nt / 8, rem = nt % 8;
+    const int x = b % 8, l = b / 8;
+    const int start = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
+    return start + l;
+}
+
+__device__ __forceinline__ double2 ld2(const double* p, long long i) {
+    return *reinterpret_cast<const double2*>(p + i);
+}
+__device__ __forceinline__ void st2(double* p, long long i, double2 v) {
+    *reinterpret_cast<double2*>(p + i) = v;
+}
+
+struct RowPair {
+    int i0, j, kb, ke, lane, w;
+    bool act, in0, in1;
+    long long idx;   // cell (i0, clamp(j), kb)
+};
+
+template <int TY>
+__device__ __forceinline__ RowPair row_pair(const SGeo& g) {
+    RowPair c;
+    const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
+    const int t = xcd_tile(blockIdx.x, nt);
+    const int tx = t % g.tiles_x;
+    const int rest = t / g.tiles_x;
+    const int ty = rest % g.tiles_y;
+    const int tz = rest / g.tiles_y;
+    c.lane = threadIdx.x & 63;
+    c.w = threadIdx.x >> 6;
+    c.i0 = tx * 128 + 2 * c.lane;
+    c.j = ty * TY + c.w;
+    c.kb = g.k0 + tz * g.kc;
+    c.ke = min(c.kb + g.kc, g.k1);
+    c.act = (c.j >= 1) && (c.j <= g.ny - 2) && (c.i0 < g.nx);
+    c.in0 = c.act && (c.i0 >= 1) && (c.i0 <= g.nx - 2);
+    c.in1 = c.act && (c.i0 + 1 <= g.nx - 2);
+    const int ic = min(c.i0, g.nx - 2 - ((g.nx - 2) & 1));  // even, in-row, 16-B aligned
+    const int jc = min(c.j, g.ny - 1);
+    c.idx = (long long)c.kb * g.ps + (long long)jc * g.px + (c.i0 < g.nx ? c.i0 : ic);
+    return c;
+}
+
+// Sweep A (iteration it):  p_it = r + beta p_{it-1} (FIRST: p = r), written
+// to pnew; (p, A p) with A p in registers; deferred x += alpha_{it-1} p_{it-1}.
+template <int TY, bool FIRST>
+__global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __restrict__ r,
+                                                 const double* __restrict__ po,
+                                                 double* __restrict__ pn, double* __restrict__ x,
+                                                 CgState* st, double* partials, unsigned* counter,
+                                                 int it) {
+    __shared__ double2 rows[2][TY + 2][64];
+    __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
     const double beta = FIRST ? 0.0 : st->beta;
-    const double alpha_prev = FIRST ? 0.0 : st->alpha;
+    const double alpha = FIRST ? 0.0 : st->alpha;
+    RowPair c = row_pair<TY>(g);
+    const bool halo = (c.w == 0) || (c.w == TY - 1);
+    const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
+    const int hslot = (c.w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - min(c.j, g.ny - 1)) * g.px;
+    const bool xok = c.i0 < g.nx;
+#define PV(ix) (FIRST ? ld2(r, ix) : [&] { double2 a_ = ld2(r, ix), b_ = ld2(po, ix); \
+        return make_double2(a_.x + beta * b_.x, a_.y + beta * b_.y); }())
+#define PS(ix) (FIRST ? r[ix] : (r[ix] + beta * po[ix]))
     double acc = 0.0;
-    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        TileCoord c = tile_coord(g, t);
-        if (!c.active) continue;
-#define PDIR(ix) (FIRST ? r[ix] : (r[ix] + beta * pold[ix]))
-        long long idx = cidx(g, c.i, c.j, c.kb);
-        double pm = PDIR(idx - g.sz);
-        double pc = PDIR(idx);
-        double poc = FIRST ? 0.0 : pold[idx];
-        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-            const long long ip = idx + g.sz;
-            double pop = FIRST ? 0.0 : pold[ip];
-            double pp = FIRST ? r[ip] : (r[ip] + beta * pop);
-            double lap = lap7(L, pc, PDIR(idx - 1), PDIR(idx + 1), PDIR(idx - g.px),
-                              PDIR(idx + g.px), pm, pp);
-            double Ap = -lap;
-            acc += pc * Ap;
-            pnew[idx] = pc;
-            if (!FIRST) x[idx] += alpha_prev * poc;
-            pm = pc;
-            pc = pp;
-            poc = pop;
+    long long idx = c.idx;
+    double2 zero = make_double2(0.0, 0.0);
+    double2 pm = xok ? PV(idx - g.sz) : zero;
+    double2 oc = (xok && !FIRST) ? ld2(po, idx) : zero;
+    double2 pc = xok ? (FIRST ? ld2(r, idx) : make_double2(ld2(r, idx).x + beta * oc.x,
+                                                          ld2(r, idx).y + beta * oc.y)) : zero;
+    double2 hc = (xok && halo) ? PV(idx + hoff) : zero;
+    int buf = 0;
+    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        const long long ip = idx + g.sz;
+        double2 op = (xok && !FIRST) ? ld2(po, ip) : zero;
+        double2 rp = xok ? ld2(r, ip) : zero;
+        double2 hp = (xok && halo && k + 1 < c.ke) ? PV(ip + hoff) : zero;
+        double2 xo = (xok && !FIRST) ? ld2(x, idx) : zero;
+        double el = (c.lane == 0 && c.i0 >= 1 && xok) ? PS(idx - 1) : 0.0;
+        double er = (c.lane == 63 && c.i0 + 2 < g.nx) ? PS(idx + 2) : 0.0;
+        rows[buf][c.w + 1][c.lane] = pc;
+        if (halo) rows[buf][hslot][c.lane] = hc;
+        __syncthreads();
+        const double2 ys = rows[buf][c.w][c.lane];
+        const double2 yn = rows[buf][c.w + 2][c.lane];
+        const double2 pp = FIRST ? rp : make_double2(rp.x + beta * op.x, rp.y + beta * op.y);
+        double left = __shfl_up(pc.y, 1, 64);
+        double right = __shfl_down(pc.x, 1, 64);
+        if (c.lane == 0) left = el;
+        if (c.lane == 63) right = er;
+        const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
+        const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
+        if (c.act) {
+            double2 pw;
+            pw.x = c.in0 ? pc.x : 0.0;
+            pw.y = c.in1 ? pc.y : 0.0;
+            st2(pn, idx, pw);
+            if (!FIRST) {
+                double2 xw;
+                xw.x = c.in0 ? xo.x + alpha * oc.x : xo.x;
+                xw.y = c.in1 ? xo.y + alpha * oc.y : xo.y;
+                st2(x, idx, xw);
+            }
         }
-#undef PDIR
+        if (c.in0) acc += pc.x * Ap0;
+        if (c.in1) acc += pc.y * Ap1;
+        pm = pc;
+        pc = pp;
+        oc = op;
+        hc = hp;
+        buf ^= 1;
     }
-    double bt = block_sum(acc, sh);
+#undef PV
+#undef PS
+    // deterministic workgroup sum: wave tree, then waves in order
+    acc = wave_sum(acc);
+    if (c.lane == 0) sh[c.w] = acc;
+    __syncthreads();
+    double bt = 0.0;
+    if (threadIdx.x == 0)
+        for (int q = 0; q < TY; ++q) bt += sh[q];
     double tot;
-    if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
+    double* shs = (double*)&rows[0][0][0];
+    if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
         st->pAp = tot;
-        if (fabs(tot) < 1e-30) {                    // CG_CHECK_BREAKDOWN(p_dot_Ap)
+        if (fabs(tot) < 1e-30) {
             st->done = 1;
             st->status = ST_STAGNATED;
             st->iterations = it + 1;
@@ -315,41 +449,68 @@ __global__ __launch_bounds__(NT) void k_cg_sweep_a(Geo g, Lap L, const double* _
     }
 }
 
-// ---------------------------------------------------------------------------
-// CG sweep B of iteration `it`: r -= alpha A p (A p recomputed from pnew,
-// bitwise equal to sweep A's), rho_new = (r, r), convergence and beta.
-// HBM per interior cell: read p, r; write r.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_cg_sweep_b(Geo g, Lap L, const double* __restrict__ p,
-                                                   double* __restrict__ r, CgState* st,
-                                                   double* partials, unsigned* counter, int it) {
-    __shared__ double sh[NWAVE];
+// Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
+// to sweep A's), rho_new = (r, r), convergence test and beta.
+template <int TY>
+__global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
+                                                 double* __restrict__ r, CgState* st,
+                                                 double* partials, unsigned* counter, int it) {
+    __shared__ double2 rows[2][TY + 2][64];
+    __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
     const double malpha = -st->alpha;
+    RowPair c = row_pair<TY>(g);
+    const bool halo = (c.w == 0) || (c.w == TY - 1);
+    const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
+    const int hslot = (c.w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - min(c.j, g.ny - 1)) * g.px;
+    const bool xok = c.i0 < g.nx;
+    const double2 zero = make_double2(0.0, 0.0);
     double acc = 0.0;
-    const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        TileCoord c = tile_coord(g, t);
-        if (!c.active) continue;
-        long long idx = cidx(g, c.i, c.j, c.kb);
-        double pm = p[idx - g.sz];
-        double pc = p[idx];
-        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-            double pp = p[idx + g.sz];
-            double lap = lap7(L, pc, p[idx - 1], p[idx + 1], p[idx - g.px], p[idx + g.px], pm, pp);
-            double Ap = -lap;
-            double rn = r[idx] + malpha * Ap;       // axpy(-alpha, Ap, r)
-            r[idx] = rn;
-            acc += rn * rn;
-            pm = pc;
-            pc = pp;
-        }
+    long long idx = c.idx;
+    double2 pm = xok ? ld2(p, idx - g.sz) : zero;
+    double2 pc = xok ? ld2(p, idx) : zero;
+    double2 hc = (xok && halo) ? ld2(p, idx + hoff) : zero;
+    int buf = 0;
+    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        const long long ip = idx + g.sz;
+        double2 pp = xok ? ld2(p, ip) : zero;
+        double2 hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
+        double2 rr = xok ? ld2(r, idx) : zero;
+        double el = (c.lane == 0 && c.i0 >= 1 && xok) ? p[idx - 1] : 0.0;
+        double er = (c.lane == 63 && c.i0 + 2 < g.nx) ? p[idx + 2] : 0.0;
+        rows[buf][c.w + 1][c.lane] = pc;
+        if (halo) rows[buf][hslot][c.lane] = hc;
+        __syncthreads();
+        const double2 ys = rows[buf][c.w][c.lane];
+        const double2 yn = rows[buf][c.w + 2][c.lane];
+        double left = __shfl_up(pc.y, 1, 64);
+        double right = __shfl_down(pc.x, 1, 64);
+        if (c.lane == 0) left = el;
+        if (c.lane == 63) right = er;
+        const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
+        const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
+        double2 rn;
+        rn.x = c.in0 ? rr.x + malpha * Ap0 : rr.x;
+        rn.y = c.in1 ? rr.y + malpha * Ap1 : rr.y;
+        if (c.act) st2(r, idx, rn);
+        if (c.in0) acc += rn.x * rn.x;
+        if (c.in1) acc += rn.y * rn.y;
+        pm = pc;
+        pc = pp;
+        hc = hp;
+        buf ^= 1;
     }
-    double bt = block_sum(acc, sh);
+    acc = wave_sum(acc);
+    if (c.lane == 0) sh[c.w] = acc;
+    __syncthreads();
+    double bt = 0.0;
+    if (threadIdx.x == 0)
+        for (int q = 0; q < TY; ++q) bt += sh[q];
     double tot;
-    if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
-        // linear_solver_cg.c:391-438
+    double* shs = (double*)&rows[0][0][0];
+    if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
         double res = sqrt(tot);
         st->res = res;
         st->iterations = it + 1;
@@ -358,7 +519,7 @@ __global__ __launch_bounds__(NT) void k_cg_sweep_b(Geo g, Lap L, const double* _
         if (check && conv) {
             st->done = 1;
             st->status = ST_CONVERGED;
-        } else if (fabs(st->rho) < 1e-30) {         // CG_CHECK_BREAKDOWN(rho)
+        } else if (fabs(st->rho) < 1e-30) {
             st->done = 1;
             st->status = ST_STAGNATED;
         } else {
@@ -366,7 +527,7 @@ __global__ __launch_bounds__(NT) void k_cg_sweep_b(Geo g, Lap L, const double* _
             st->rho = tot;
             if (it + 1 >= st->max_iter) {
                 st->done = 1;
-                st->status = conv ? ST_CONVERGED : ST_MAX_ITER;  // final check, cg.c:441-443
+                st->status = conv ? ST_CONVERGED : ST_MAX_ITER;
             }
         }
     }

@@ -60,6 +60,8 @@ struct hip_proj_ctx {
     size_t nx = 0, ny = 0, nz = 0;
     long long px = 0, ps = 0;
     Geo geo{};
+    SGeo sgeo{};       // row-pair CG sweep tiling
+    int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
     int grid_cap = 2048;
     hip_proj_config_t cfg{};
     // fields
@@ -159,6 +161,40 @@ static int tile_grid(const hip_proj_ctx* c) {
     return (int)std::max(1LL, std::min<long long>(nt, c->grid_cap));
 }
 
+static int sweep_grid(const hip_proj_ctx* c) {
+    return c->sgeo.tiles_x * c->sgeo.tiles_y * c->sgeo.tiles_z;
+}
+
+static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
+                       const double* po, double* pn, double* x, int it) {
+    const dim3 grid(sweep_grid(c)), block(64 * c->sweep_ty);
+    if (c->sweep_ty == 4) {
+        if (first)
+            hipLaunchKernelGGL((k_cgA<4, true>), grid, block, 0, c->stream, c->sgeo, L, r, po, pn,
+                               x, c->st, c->partials, c->counter, it);
+        else
+            hipLaunchKernelGGL((k_cgA<4, false>), grid, block, 0, c->stream, c->sgeo, L, r, po,
+                               pn, x, c->st, c->partials, c->counter, it);
+    } else {
+        if (first)
+            hipLaunchKernelGGL((k_cgA<8, true>), grid, block, 0, c->stream, c->sgeo, L, r, po, pn,
+                               x, c->st, c->partials, c->counter, it);
+        else
+            hipLaunchKernelGGL((k_cgA<8, false>), grid, block, 0, c->stream, c->sgeo, L, r, po,
+                               pn, x, c->st, c->partials, c->counter, it);
+    }
+}
+
+static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
+    const dim3 grid(sweep_grid(c)), block(64 * c->sweep_ty);
+    if (c->sweep_ty == 4)
+        hipLaunchKernelGGL((k_cgB<4>), grid, block, 0, c->stream, c->sgeo, L, p, r, c->st,
+                           c->partials, c->counter, it);
+    else
+        hipLaunchKernelGGL((k_cgB<8>), grid, block, 0, c->stream, c->sgeo, L, p, r, c->st,
+                           c->partials, c->counter, it);
+}
+
 static dim3 cell_grid(const hip_proj_ctx* c) {
     return dim3((unsigned)((c->nx + 63) / 64), (unsigned)((c->ny + 3) / 4), (unsigned)c->nz);
 }
@@ -229,14 +265,8 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     double* P[2] = {c->pa, c->pb};
     int it = 0;
     if (max_iter > 0) {
-        timed(c, HIP_KT_CG_SWEEP_A, [&] {
-            hipLaunchKernelGGL(k_cg_sweep_a<true>, dim3(G), dim3(NT), 0, c->stream, c->geo, L,
-                               c->r, P[1], P[0], x, c->st, c->partials, c->counter, 0);
-        });
-        timed(c, HIP_KT_CG_SWEEP_B, [&] {
-            hipLaunchKernelGGL(k_cg_sweep_b, dim3(G), dim3(NT), 0, c->stream, c->geo, L, P[0],
-                               c->r, c->st, c->partials, c->counter, 0);
-        });
+        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, true, L, c->r, P[1], P[0], x, 0); });
+        timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, P[0], c->r, 0); });
         it = 1;
     }
     int chunk = 8;
@@ -247,14 +277,8 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         for (int q = 0; q < n; ++q, ++it) {
             double* pnew = P[it & 1];
             double* pold = P[(it + 1) & 1];
-            timed(c, HIP_KT_CG_SWEEP_A, [&] {
-                hipLaunchKernelGGL(k_cg_sweep_a<false>, dim3(G), dim3(NT), 0, c->stream, c->geo,
-                                   L, c->r, pold, pnew, x, c->st, c->partials, c->counter, it);
-            });
-            timed(c, HIP_KT_CG_SWEEP_B, [&] {
-                hipLaunchKernelGGL(k_cg_sweep_b, dim3(G), dim3(NT), 0, c->stream, c->geo, L,
-                                   pnew, c->r, c->st, c->partials, c->counter, it);
-            });
+            timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, false, L, c->r, pold, pnew, x, it); });
+            timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); });
         }
         HIP_TRY(hipMemcpyAsync(&c->h_state[slot], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
                                c->stream));
@@ -436,6 +460,7 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.poll_interval = 64;
     c.kchunk = 0;
     c.verbose = 0;
+    c.sweep_rows = 8;
     return c;
 }
 
@@ -486,7 +511,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     g.k0 = (nz > 1) ? 1 : 0;
     g.k1 = (nz > 1) ? (int)nz - 1 : 1;
     const int nint_k = g.k1 - g.k0;
-    int kc = c->cfg.kchunk;
+    int kc = 0;
     if (kc <= 0) {
         // enough tiles to fill every CU several times, long z runs otherwise
         long long xy_tiles = (long long)((nx + TX - 1) / TX) * (long long)((ny + TY - 1) / TY);
@@ -499,6 +524,24 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     g.tiles_y = (int)((ny + TY - 1) / TY);
     g.tiles_z = (nint_k + g.kc - 1) / g.kc;
 
+    // row-pair CG sweeps: 128 x TY x kc tiles (kernels.hpp, k_cgA / k_cgB)
+    c->sweep_ty = (c->cfg.sweep_rows == 4) ? 4 : 8;
+    SGeo& sg = c->sgeo;
+    sg.nx = g.nx;
+    sg.ny = g.ny;
+    sg.nz = g.nz;
+    sg.px = g.px;
+    sg.ps = g.ps;
+    sg.sz = g.sz;
+    sg.k0 = g.k0;
+    sg.k1 = g.k1;
+    sg.kc = (c->cfg.kchunk > 0) ? c->cfg.kchunk : 64;
+    sg.kc = std::max(1, std::min(sg.kc, nint_k));
+    sg.tiles_x = (int)((nx + 127) / 128);
+    sg.tiles_y = (int)((ny + c->sweep_ty - 1) / c->sweep_ty);
+    sg.tiles_z = (nint_k + sg.kc - 1) / sg.kc;
+    const int n_partials = std::max(c->grid_cap, sg.tiles_x * sg.tiles_y * sg.tiles_z);
+
     const size_t n = field_elems(c);
     double** fields[] = {&c->u, &c->v, &c->w, &c->p, &c->us, &c->vs, &c->ws, &c->pn,
                          &c->r, &c->pa, &c->pb};
@@ -510,7 +553,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     if (dalloc(c, &c->src_v_col, nx) != CFD_SUCCESS) return CFD_ERROR;
     HIP_TRY(hipMalloc((void**)&c->st, sizeof(CgState)));
     HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
-    HIP_TRY(hipMalloc((void**)&c->partials, sizeof(double) * c->grid_cap));
+    HIP_TRY(hipMalloc((void**)&c->partials, sizeof(double) * n_partials));
     HIP_TRY(hipMalloc((void**)&c->counter, 64));
     HIP_TRY(hipMemsetAsync(c->counter, 0, 64, c->stream));
     HIP_TRY(hipMalloc((void**)&c->red, 8 * sizeof(unsigned long long)));

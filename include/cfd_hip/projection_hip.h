@@ -55,8 +55,9 @@ typedef struct {
     int poisson_check_interval;   /* convergence check period (1) */
     double sor_omega;             /* <= 0: optimal omega (linear_solver_internal.h:184-220) */
     int poll_interval;            /* iterations launched between host convergence polls */
-    int kchunk;                   /* z planes per stencil tile; 0 = auto */
+    int kchunk;                   /* z planes per CG sweep tile; 0 = auto (64) */
     int verbose;
+    int sweep_rows;               /* y rows (wavefronts) per CG sweep workgroup: 4 or 8 */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
