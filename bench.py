@@ -11,7 +11,11 @@ corrector). value = interior cells updated per second over all ranks, in
 MLUPS.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-For N > 1 launch with torch.distributed.run (one rank per GPU).
+For N > 1 launch with torch.distributed.run (one rank per GPU): the grid is
+split into N Z-slabs (hip_proj_create_slab), halo planes and CG dot products
+move over RCCL (a communicator our library creates from a unique id that
+rank 0 broadcasts over a gloo group), and the total work is fixed, so the
+scaling is strong.
 """
 from __future__ import annotations
 
@@ -71,14 +75,18 @@ def main():
     lib = _native.hip()
     if lib.hip_projection_available() != 1:
         raise SystemExit("bench: no HIP device")
-    if world > 1:
-        raise SystemExit("bench: multi-GPU Z-slab path not built yet")
+    torch.cuda.set_device(local)
 
     n = args.n
     nu = 1.0 / args.re
     g = api.Grid(n, n, n, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
     params = api.validation_params(args.dt, nu)
-    ctx = api.HipProjection(n, n, n, device=local, kchunk=args.kchunk,
+    comm = None
+    if world > 1:
+        uid = [api.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = api.SlabComm.rccl(uid[0], rank, world, local)
+    ctx = api.HipProjection(n, n, n, comm=comm, device=local, kchunk=args.kchunk,
                              sweep_rows=args.sweep_rows)
     for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
         ctx.fill(fid, 0.0)
@@ -119,21 +127,24 @@ def main():
         elapsed = float(tt[0])
 
     n_int = (n - 2) ** 3
+    n_loc = (n - 2) ** 2 * (ctx.nz_local - 2)  # interior cells of this rank's slab
     ms_step = elapsed / args.steps * 1e3
-    mlups = n_int * args.steps * world / elapsed / 1e6
+    # strong scaling: the ranks share one n^3 grid, so the job updates n_int
+    # cells per step whatever the rank count
+    mlups = n_int * args.steps / elapsed / 1e6
     k_mean = sum(iters) / len(iters)
     step_bytes = (BYTES_STEP_FIXED_SURVEY + BYTES_CG_ITER_SURVEY * k_mean) * n_int
-    gbps_step = step_bytes * args.steps * world / elapsed / 1e9
+    gbps_step = step_bytes * args.steps / elapsed / 1e9
 
     kt = ctx.timing()
     ms_a, n_a = kt["cg_sweep_a"]
     ms_b, n_b = kt["cg_sweep_b"]
     avg_a = ms_a / max(n_a, 1)
     avg_b = ms_b / max(n_b, 1)
-    ach_a = BYTES_SWEEP_A * n_int / (avg_a * 1e-3) / 1e9 if n_a else None
-    ach_b = BYTES_SWEEP_B * n_int / (avg_b * 1e-3) / 1e9 if n_b else None
+    ach_a = BYTES_SWEEP_A * n_loc / (avg_a * 1e-3) / 1e9 if n_a else None
+    ach_b = BYTES_SWEEP_B * n_loc / (avg_b * 1e-3) / 1e9 if n_b else None
     cg_iter_ms = avg_a + avg_b
-    cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_int / (cg_iter_ms * 1e-3) / 1e9
+    cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_loc / (cg_iter_ms * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -156,7 +167,8 @@ def main():
             "config": {"workload": f"{n}^3 lid-driven cavity Re={args.re:g}, dt={args.dt:g}, "
                                    "projection_hip (CG rel 1e-6)",
                        "grid": [n, n, n], "interior_cells": n_int,
-                       "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"z-slab x{world} (RCCL halo + allreduce)" if world > 1
+                       else "single GPU"},
             "achieved_GBps": round(gbps_step, 1),
             "cg_iters_per_step": iters,
             "cg_iter_ms": round(cg_iter_ms, 4),
@@ -176,6 +188,8 @@ def main():
         }
         print(json.dumps(out))
     ctx.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

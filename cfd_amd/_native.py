@@ -126,6 +126,20 @@ def _bind_hip(lib) -> None:
          C.c_double, C.c_int)
     _sig(lib, "hip_proj_poisson_solve", C.c_int, V, C.c_int, A.c_double_p, A.c_double_p,
          C.c_double, C.c_double, C.c_double, P(A.PoissonParams), P(A.PoissonStats))
+    _sig(lib, "hip_proj_slab_layout", C.c_int, C.c_size_t, C.c_int, C.c_int, P(C.c_size_t),
+         P(C.c_size_t))
+    _sig(lib, "hip_proj_comm_unique_id", C.c_int, C.c_char_p)
+    _sig(lib, "hip_proj_comm_create_rccl", V, C.c_char_p, C.c_int, C.c_int, C.c_int)
+    _sig(lib, "hip_proj_group_create", V, C.c_int)
+    _sig(lib, "hip_proj_group_destroy", None, V)
+    _sig(lib, "hip_proj_comm_create_local", V, V, C.c_int, C.c_int)
+    _sig(lib, "hip_proj_comm_destroy", None, V)
+    _sig(lib, "hip_proj_comm_rank", C.c_int, V)
+    _sig(lib, "hip_proj_comm_size", C.c_int, V)
+    _sig(lib, "hip_proj_create_slab", V, C.c_size_t, C.c_size_t, C.c_size_t, V,
+         P(A.HipProjConfig))
+    _sig(lib, "hip_proj_slab_info", C.c_int, V, P(C.c_size_t), P(C.c_size_t), P(C.c_int),
+         P(C.c_int))
     _sig(lib, "create_projection_hip_solver", P(A.NSSolver))
     _sig(lib, "cfd_hip_register_solvers", None, V)
 

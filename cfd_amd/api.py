@@ -279,16 +279,143 @@ def hip_config(**kw) -> A.HipProjConfig:
     return cfg
 
 
-class HipProjection:
-    """Device-resident projection context (hip_proj_* C-ABI)."""
+def slab_layout(nz: int, rank: int, size: int):
+    """(k_offset, nz_local) of `rank`'s Z-slab (hip_proj_slab_layout; host only)."""
+    ko, nl = C.c_size_t(), C.c_size_t()
+    _check(_native.hip().hip_proj_slab_layout(nz, rank, size, C.byref(ko), C.byref(nl)),
+           "hip_proj_slab_layout")
+    return ko.value, nl.value
 
-    def __init__(self, nx, ny, nz=1, **config):
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id bytes (rank 0 creates, the caller broadcasts)."""
+    buf = C.create_string_buffer(128)
+    _check(_native.hip().hip_proj_comm_unique_id(buf), "hip_proj_comm_unique_id")
+    return buf.raw
+
+
+class SlabComm:
+    """One rank's Z-slab communicator (RCCL or in-process group endpoint)."""
+
+    def __init__(self, handle, keepalive=None):
+        if not handle:
+            raise CfdError(_native.host().cfd_get_last_status(), "slab comm create")
+        self._h = handle
+        self._keep = keepalive
+
+    @classmethod
+    def rccl(cls, uid: bytes, rank: int, size: int, device: int = 0) -> "SlabComm":
+        assert len(uid) == 128
+        return cls(_native.hip().hip_proj_comm_create_rccl(uid, rank, size, device))
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def rank(self) -> int:
+        return _native.hip().hip_proj_comm_rank(self._h)
+
+    @property
+    def size(self) -> int:
+        return _native.hip().hip_proj_comm_size(self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _native.hip().hip_proj_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LocalGroup:
+    """In-process slab group: `size` ranks driven by host threads of this
+    process (hip_proj_group_*); see run_ranks()."""
+
+    def __init__(self, size: int):
+        self._g = _native.hip().hip_proj_group_create(size)
+        if not self._g:
+            raise CfdError(_native.host().cfd_get_last_status(), "hip_proj_group_create")
+        self.size = size
+        self.comms = []
+
+    def comm(self, rank: int, device: int = 0) -> SlabComm:
+        c = SlabComm(_native.hip().hip_proj_comm_create_local(self._g, rank, device), self)
+        self.comms.append(c)
+        return c
+
+    def close(self):
+        for c in self.comms:
+            c.close()
+        self.comms = []
+        if getattr(self, "_g", None):
+            _native.hip().hip_proj_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_ranks(fn, n: int):
+    """Run fn(rank) on n host threads (ctypes drops the GIL inside the C calls)
+    and return the results in rank order; re-raises the first exception."""
+    import threading
+
+    out = [None] * n
+    err = [None] * n
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001
+            err[r] = e
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return out
+
+
+class HipProjection:
+    """Device-resident projection context (hip_proj_* C-ABI). With `comm`, the
+    context holds rank comm.rank's Z-slab of the global nx*ny*nz grid and its
+    fields have shape (nz_local, ny, nx)."""
+
+    def __init__(self, nx, ny, nz=1, comm: Optional[SlabComm] = None, **config):
         lib = _native.hip()
         self._cfg = hip_config(**config)
-        self.shape = (nz, ny, nx)
-        self._ctx = lib.hip_proj_create(nx, ny, nz, C.byref(self._cfg))
+        self._comm = comm
+        if comm is None:
+            self._ctx = lib.hip_proj_create(nx, ny, nz, C.byref(self._cfg))
+        else:
+            self._ctx = lib.hip_proj_create_slab(nx, ny, nz, comm.handle, C.byref(self._cfg))
         if not self._ctx:
             raise CfdError(_native.host().cfd_get_last_status(), "hip_proj_create")
+        ko, nl = C.c_size_t(), C.c_size_t()
+        rk, sz = C.c_int(), C.c_int()
+        lib.hip_proj_slab_info(self._ctx, C.byref(ko), C.byref(nl), C.byref(rk), C.byref(sz))
+        self.k_offset, self.nz_local, self.rank, self.size = ko.value, nl.value, rk.value, sz.value
+        self.nz_global = nz
+        self.shape = (nl.value, ny, nx)
+
+    def owned(self):
+        """(local, global) plane slices this rank is authoritative for: its
+        interior planes plus the global z faces it holds."""
+        lo = 0 if self.rank == 0 else 1
+        hi = self.nz_local if self.rank == self.size - 1 else self.nz_local - 1
+        return slice(lo, hi), slice(self.k_offset + lo, self.k_offset + hi)
 
     @property
     def ctx(self):

@@ -48,6 +48,8 @@ struct Geo {
     int k0, k1;            // interior planes [k0, k1)
     int kc;                // planes per tile
     int tiles_x, tiles_y, tiles_z;
+    int lo_face, hi_face;  // local plane 0 / nz-1 is a global z face (Z-slabs: edge ranks)
+    int kofs;              // global index of local plane 0 (Z-slabs)
 };
 
 struct Lap {
@@ -201,6 +203,85 @@ __device__ __forceinline__ double lap7(const Lap& L, double c, double xm, double
 }
 
 // ---------------------------------------------------------------------------
+// CG state transitions, run by one thread once a dot product's global total is
+// known: inline in the last workgroup on one device, or in a 1-thread k_finish_*
+// kernel after the cross-rank all-reduce of the per-rank totals (Z-slabs).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fin_setup(CgState* st, double tot, double rel_tol, double abs_tol,
+                                          int max_iter, int check_interval) {
+    double res0 = sqrt(tot);                   // linear_solver_cg.c:345
+    double tol = rel_tol * res0;               // :352-355
+    if (tol < abs_tol) tol = abs_tol;
+    st->rho = tot;
+    st->res0 = res0;
+    st->res = res0;
+    st->tol = tol;
+    st->abs_tol = abs_tol;
+    st->alpha = 0.0;
+    st->beta = 0.0;
+    st->pAp = 0.0;
+    st->iterations = 0;
+    st->pending = 0;
+    st->max_iter = max_iter;
+    st->check_interval = check_interval;
+    if (res0 < abs_tol || max_iter <= 0) {     // :357-365
+        st->done = 1;
+        st->status = (res0 < abs_tol) ? ST_CONVERGED : ST_MAX_ITER;
+    } else {
+        st->done = 0;
+        st->status = ST_MAX_ITER;
+    }
+}
+
+// after (p, Ap): alpha or pAp breakdown (linear_solver_cg.c:395-407)
+__device__ __forceinline__ void fin_A(CgState* st, double tot, int it) {
+    st->pAp = tot;
+    if (fabs(tot) < 1e-30) {
+        st->done = 1;
+        st->status = ST_STAGNATED;
+        st->iterations = it + 1;
+        st->pending = 0;
+    } else {
+        st->alpha = st->rho / tot;
+        st->pending = 1;
+    }
+}
+
+// after (r, r): convergence test, rho breakdown, beta (linear_solver_cg.c:416-445)
+__device__ __forceinline__ void fin_B(CgState* st, double tot, int it) {
+    double res = sqrt(tot);
+    st->res = res;
+    st->iterations = it + 1;
+    const bool check = (it % st->check_interval) == 0;
+    const bool conv = (res < st->tol) || (res < st->abs_tol);
+    if (check && conv) {
+        st->done = 1;
+        st->status = ST_CONVERGED;
+    } else if (fabs(st->rho) < 1e-30) {
+        st->done = 1;
+        st->status = ST_STAGNATED;
+    } else {
+        st->beta = tot / st->rho;
+        st->rho = tot;
+        if (it + 1 >= st->max_iter) {
+            st->done = 1;
+            st->status = conv ? ST_CONVERGED : ST_MAX_ITER;
+        }
+    }
+}
+
+__global__ void k_finish_setup(CgState* st, const double* tot, double rel_tol, double abs_tol,
+                               int max_iter, int check_interval) {
+    if (threadIdx.x == 0) fin_setup(st, tot[0], rel_tol, abs_tol, max_iter, check_interval);
+}
+__global__ void k_finish_A(CgState* st, const double* tot, int it) {
+    if (threadIdx.x == 0 && !st->done) fin_A(st, tot[0], it);
+}
+__global__ void k_finish_B(CgState* st, const double* tot, int it) {
+    if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it);
+}
+
+// ---------------------------------------------------------------------------
 // CG setup: r = -rhs + lap(x) (linear_solver_cg.c:134-158) and rho = (r, r).
 // FROM_VEL: rhs = (rho/dt) * div(u*) computed on the fly exactly as
 // solver_projection.c:195-214 (the rhs array is never materialised for CG);
@@ -213,7 +294,7 @@ struct DivCoef {
     double rho_over_dt;
 };
 
-template <bool FROM_VEL, bool WRITE_RHS, bool WITH_RR>
+template <bool FROM_VEL, bool WRITE_RHS, bool WITH_RR, bool DIST = false>
 __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
                                                  const double* __restrict__ us,
                                                  const double* __restrict__ vs,
@@ -223,7 +304,7 @@ __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
                                                  double* __restrict__ r, CgState* st,
                                                  double* partials, unsigned* counter,
                                                  double rel_tol, double abs_tol, int max_iter,
-                                                 int check_interval) {
+                                                 int check_interval, double* dsum) {
     __shared__ double sh[NWAVE];
     __shared__ int flag;
     double acc = 0.0;
@@ -260,28 +341,8 @@ __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
     double bt = block_sum(acc, sh);
     double tot;
     if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
-        double res0 = sqrt(tot);                   // linear_solver_cg.c:345
-        double tol = rel_tol * res0;               // :352-355
-        if (tol < abs_tol) tol = abs_tol;
-        st->rho = tot;
-        st->res0 = res0;
-        st->res = res0;
-        st->tol = tol;
-        st->abs_tol = abs_tol;
-        st->alpha = 0.0;
-        st->beta = 0.0;
-        st->pAp = 0.0;
-        st->iterations = 0;
-        st->pending = 0;
-        st->max_iter = max_iter;
-        st->check_interval = check_interval;
-        if (res0 < abs_tol || max_iter <= 0) {     // :357-365
-            st->done = 1;
-            st->status = (res0 < abs_tol) ? ST_CONVERGED : ST_MAX_ITER;
-        } else {
-            st->done = 0;
-            st->status = ST_MAX_ITER;
-        }
+        if (DIST) dsum[0] = tot;
+        else fin_setup(st, tot, rel_tol, abs_tol, max_iter, check_interval);
     }
 }
 
@@ -354,12 +415,12 @@ __device__ __forceinline__ RowPair row_pair(const SGeo& g) {
 
 // Sweep A (iteration it):  p_it = r + beta p_{it-1} (FIRST: p = r), written
 // to pnew; (p, A p) with A p in registers; deferred x += alpha_{it-1} p_{it-1}.
-template <int TY, bool FIRST>
+template <int TY, bool FIRST, bool DIST>
 __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __restrict__ r,
                                                  const double* __restrict__ po,
                                                  double* __restrict__ pn, double* __restrict__ x,
                                                  CgState* st, double* partials, unsigned* counter,
-                                                 int it) {
+                                                 int it, double* dsum) {
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
@@ -436,25 +497,18 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
     double tot;
     double* shs = (double*)&rows[0][0][0];
     if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
-        st->pAp = tot;
-        if (fabs(tot) < 1e-30) {
-            st->done = 1;
-            st->status = ST_STAGNATED;
-            st->iterations = it + 1;
-            st->pending = 0;
-        } else {
-            st->alpha = st->rho / tot;
-            st->pending = 1;
-        }
+        if (DIST) dsum[0] = tot;
+        else fin_A(st, tot, it);
     }
 }
 
 // Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
 // to sweep A's), rho_new = (r, r), convergence test and beta.
-template <int TY>
+template <int TY, bool DIST>
 __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
                                                  double* __restrict__ r, CgState* st,
-                                                 double* partials, unsigned* counter, int it) {
+                                                 double* partials, unsigned* counter, int it,
+                                                 double* dsum) {
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
@@ -511,25 +565,8 @@ __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __
     double tot;
     double* shs = (double*)&rows[0][0][0];
     if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
-        double res = sqrt(tot);
-        st->res = res;
-        st->iterations = it + 1;
-        const bool check = (it % st->check_interval) == 0;
-        const bool conv = (res < st->tol) || (res < st->abs_tol);
-        if (check && conv) {
-            st->done = 1;
-            st->status = ST_CONVERGED;
-        } else if (fabs(st->rho) < 1e-30) {
-            st->done = 1;
-            st->status = ST_STAGNATED;
-        } else {
-            st->beta = tot / st->rho;
-            st->rho = tot;
-            if (it + 1 >= st->max_iter) {
-                st->done = 1;
-                st->status = conv ? ST_CONVERGED : ST_MAX_ITER;
-            }
-        }
+        if (DIST) dsum[0] = tot;
+        else fin_B(st, tot, it);
     }
 }
 
@@ -550,10 +587,6 @@ __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, const double* __restr
     }
 }
 
-// Fixed-iteration CG microbenchmark variants: same sweeps, no early exit.
-// (They reuse k_cg_sweep_a / k_cg_sweep_b with max_iter set huge and the
-// convergence test disabled by a zero tolerance.)
-
 // ---------------------------------------------------------------------------
 // Boundary conditions as pure gathers from interior cells (race-free):
 //   Neumann  (boundary_conditions_core_impl.h:41-85): c -> clamp(c, 1, n-2)
@@ -573,12 +606,17 @@ __device__ __forceinline__ int bc_map(int c, int n, int mode) {
     return c == 0 ? n - 2 : (c == n - 1 ? 1 : c);
 }
 
+// In a Z-slab the z faces exist only on the edge ranks (lo_face / hi_face);
+// the x/y ring is applied on every local plane, halo planes included (their
+// owner applies the identical gather to the same values).
 __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f, int mode,
                                                   DirVals dv) {
     const bool is3d = g.nz > 1;
+    const bool lo = is3d && g.lo_face, hi = is3d && g.hi_face;
     const long long ring = 2LL * g.nx + 2LL * (g.ny - 2);  // x/y boundary ring of one plane
     const long long nring = ring * g.nz;
-    const long long nzf = is3d ? 2LL * g.nx * g.ny : 0;    // two full z planes
+    const long long plane = (long long)g.nx * g.ny;
+    const long long nzf = (lo ? plane : 0) + (hi ? plane : 0);
     const long long total = nring + nzf;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (long long)gridDim.x * blockDim.x) {
@@ -592,17 +630,17 @@ __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f,
             else { i = g.nx - 1; j = (int)(q - 2LL * g.nx - (g.ny - 2)) + 1; }
         } else {
             long long q = e - nring;
-            long long plane = (long long)g.nx * g.ny;
-            k = (q < plane) ? 0 : g.nz - 1;
+            k = (lo && q < plane) ? 0 : g.nz - 1;
             q = q % plane;
             j = (int)(q / g.nx);
             i = (int)(q % g.nx);
         }
+        const bool zlo = lo && k == 0, zhi = hi && k == g.nz - 1;
         const long long dst = cidx(g, i, j, k);
         if (mode == 2) {
             double v;
-            if (is3d && k == 0) v = dv.back;
-            else if (is3d && k == g.nz - 1) v = dv.front;
+            if (zlo) v = dv.back;
+            else if (zhi) v = dv.front;
             else if (j == 0) v = dv.bottom;
             else if (j == g.ny - 1) v = dv.top;
             else if (i == 0) v = dv.left;
@@ -610,7 +648,7 @@ __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f,
             f[dst] = v;
         } else {
             int si = bc_map(i, g.nx, mode), sj = bc_map(j, g.ny, mode);
-            int sk = is3d ? bc_map(k, g.nz, mode) : k;
+            int sk = (zlo || zhi) ? bc_map(k, g.nz, mode) : k;
             f[dst] = f[cidx(g, si, sj, sk)];
         }
     }
@@ -711,6 +749,7 @@ struct CorrCoef {
     double two_dx, two_dy, inv_2dz;
     double dt_over_rho;
 };
+constexpr int CORR_KC = 64;  // planes per corrector workgroup
 
 __global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
                                                    const double* __restrict__ us,
@@ -726,9 +765,15 @@ __global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
     __syncthreads();
     const int i = blockIdx.x * 64 + (threadIdx.x & 63);
     const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int k = blockIdx.z;
+    // each workgroup walks a chunk of planes: few workgroups -> few atomics.
+    // Planes [ks, ke): the owned planes plus the global z faces; a Z-slab's
+    // halo planes belong to the neighbour and are left out of the maxima.
+    const int ks = (g.nz > 1 && !g.lo_face) ? 1 : 0;
+    const int ke = (g.nz > 1 && !g.hi_face) ? g.nz - 1 : g.nz;
+    const int kbeg = ks + blockIdx.z * CORR_KC, kend = min(kbeg + CORR_KC, ke);
     double mv = 0.0, mp = 0.0;
-    if (i < g.nx && j < g.ny) {
+    if (i < g.nx && j < g.ny)
+    for (int k = kbeg; k < kend; ++k) {
         const long long idx = cidx(g, i, j, k);
         const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
                                k >= g.k0 && k < g.k1);
@@ -815,7 +860,7 @@ __global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __r
         if (!c.active) continue;
         long long idx = cidx(g, c.i, c.j, c.kb);
         for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-            if (((c.i + c.j + k) & 1) != parity) continue;
+            if (((c.i + c.j + k + g.kofs) & 1) != parity) continue;  // global parity
             double pn = -(rhs[idx] - (x[idx + 1] + x[idx - 1]) / rc.dx2 -
                           (x[idx + g.px] + x[idx - g.px]) / rc.dy2 -
                           (x[idx + g.sz] + x[idx - g.sz]) * rc.inv_dz2) *

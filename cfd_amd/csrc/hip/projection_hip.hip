@@ -10,6 +10,7 @@
 // is no host round trip per iteration (the reference GPU path does two per
 // iteration, poisson_cg_gpu_solve.cuh:189-203).
 #include "kernels.hpp"
+#include "slab_comm.hpp"
 
 #include "cfd_hip/projection_hip.h"
 
@@ -20,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <vector>
 
 using namespace cfdhip;
@@ -64,6 +66,13 @@ struct hip_proj_ctx {
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
     int grid_cap = 2048;
     hip_proj_config_t cfg{};
+    // Z-slab decomposition (nranks == 1: the whole grid, no communicator)
+    SlabComm* comm = nullptr;
+    int rank = 0, nranks = 1;
+    size_t nzg = 0;    // global nz
+    size_t kofs = 0;   // global index of local plane 0
+    double* dsum = nullptr;            // [0] local dot total, [1] all-reduced
+    unsigned long long* redg = nullptr;  // all-reduced red[]
     // fields
     double *u = nullptr, *v = nullptr, *w = nullptr, *p = nullptr, *T = nullptr;
     double *us = nullptr, *vs = nullptr, *ws = nullptr, *pn = nullptr;
@@ -165,34 +174,41 @@ static int sweep_grid(const hip_proj_ctx* c) {
     return c->sgeo.tiles_x * c->sgeo.tiles_y * c->sgeo.tiles_z;
 }
 
+static bool dist(const hip_proj_ctx* c) { return c->nranks > 1; }
+
+template <int TY, bool FIRST, bool DIST>
+static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
+                         double* pn, double* x, int it) {
+    hipLaunchKernelGGL((k_cgA<TY, FIRST, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream,
+                       c->sgeo, L, r, po, pn, x, c->st, c->partials, c->counter, it, c->dsum);
+}
+
+template <int TY, bool DIST>
+static void launch_cgB_t(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
+    hipLaunchKernelGGL((k_cgB<TY, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream,
+                       c->sgeo, L, p, r, c->st, c->partials, c->counter, it, c->dsum);
+}
+
 static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
                        const double* po, double* pn, double* x, int it) {
-    const dim3 grid(sweep_grid(c)), block(64 * c->sweep_ty);
+    const bool d = dist(c);
     if (c->sweep_ty == 4) {
-        if (first)
-            hipLaunchKernelGGL((k_cgA<4, true>), grid, block, 0, c->stream, c->sgeo, L, r, po, pn,
-                               x, c->st, c->partials, c->counter, it);
-        else
-            hipLaunchKernelGGL((k_cgA<4, false>), grid, block, 0, c->stream, c->sgeo, L, r, po,
-                               pn, x, c->st, c->partials, c->counter, it);
+        if (first) d ? launch_cgA_t<4, true, true>(c, L, r, po, pn, x, it)
+                     : launch_cgA_t<4, true, false>(c, L, r, po, pn, x, it);
+        else d ? launch_cgA_t<4, false, true>(c, L, r, po, pn, x, it)
+               : launch_cgA_t<4, false, false>(c, L, r, po, pn, x, it);
     } else {
-        if (first)
-            hipLaunchKernelGGL((k_cgA<8, true>), grid, block, 0, c->stream, c->sgeo, L, r, po, pn,
-                               x, c->st, c->partials, c->counter, it);
-        else
-            hipLaunchKernelGGL((k_cgA<8, false>), grid, block, 0, c->stream, c->sgeo, L, r, po,
-                               pn, x, c->st, c->partials, c->counter, it);
+        if (first) d ? launch_cgA_t<8, true, true>(c, L, r, po, pn, x, it)
+                     : launch_cgA_t<8, true, false>(c, L, r, po, pn, x, it);
+        else d ? launch_cgA_t<8, false, true>(c, L, r, po, pn, x, it)
+               : launch_cgA_t<8, false, false>(c, L, r, po, pn, x, it);
     }
 }
 
 static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    const dim3 grid(sweep_grid(c)), block(64 * c->sweep_ty);
-    if (c->sweep_ty == 4)
-        hipLaunchKernelGGL((k_cgB<4>), grid, block, 0, c->stream, c->sgeo, L, p, r, c->st,
-                           c->partials, c->counter, it);
-    else
-        hipLaunchKernelGGL((k_cgB<8>), grid, block, 0, c->stream, c->sgeo, L, p, r, c->st,
-                           c->partials, c->counter, it);
+    const bool d = dist(c);
+    if (c->sweep_ty == 4) d ? launch_cgB_t<4, true>(c, L, p, r, it) : launch_cgB_t<4, false>(c, L, p, r, it);
+    else d ? launch_cgB_t<8, true>(c, L, p, r, it) : launch_cgB_t<8, false>(c, L, p, r, it);
 }
 
 static dim3 cell_grid(const hip_proj_ctx* c) {
@@ -236,6 +252,35 @@ static Lap make_lap(double dx, double dy, double dz) {
     return L;
 }
 
+// Refresh the halo planes of the given slab fields (no-op on one rank).
+static cfd_status_t halo(hip_proj_ctx* c, std::initializer_list<double*> fs,
+                         bool periodic = false) {
+    if (!dist(c)) return CFD_SUCCESS;
+    double* f[8];
+    int n = 0;
+    for (double* x : fs) f[n++] = x;
+    return c->comm->halo(c->stream, f, n, c->ps, (int)c->nz, periodic);
+}
+
+// Sum the per-rank dot total dsum[0] into dsum[1].
+static cfd_status_t reduce_dot(hip_proj_ctx* c) {
+    return c->comm->allreduce_sum(c->stream, c->dsum, c->dsum + 1, 1);
+}
+
+// Device copy of the maxima/flags in red[] that every rank agrees on.
+static const unsigned long long* reduce_red(hip_proj_ctx* c, cfd_status_t* st) {
+    *st = CFD_SUCCESS;
+    if (!dist(c)) return c->red;
+    *st = c->comm->allreduce_max_u64(c->stream, c->red, c->redg, 8);
+    return c->redg;
+}
+
+#define ST_TRY(expr)                            \
+    do {                                        \
+        cfd_status_t s_ = (expr);               \
+        if (s_ != CFD_SUCCESS) return s_;       \
+    } while (0)
+
 // ---------------------------------------------------------------------------
 // pressure solvers on ctx->pn
 // ---------------------------------------------------------------------------
@@ -247,39 +292,77 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     const Lap L = make_lap(dx, dy, dz);
     const int G = tile_grid(c);
     const DirVals dv{};
+    const bool D = dist(c);
     double* x = c->pn;
+    ST_TRY(halo(c, {x}));
     // poisson_solver_apply_bc(x) at solve start (linear_solver_cg.c:320)
     launch_bc(c, x, 0, dv);
     timed(c, HIP_KT_CG_SETUP, [&] {
-        if (src == RHS_FROM_VELOCITY)
-            hipLaunchKernelGGL((k_cg_setup<true, false, true>), dim3(G), dim3(NT), 0, c->stream,
-                               c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x, c->r, c->st,
-                               c->partials, c->counter, rel_tol, abs_tol, max_iter,
-                               check_interval);
-        else
-            hipLaunchKernelGGL((k_cg_setup<false, false, true>), dim3(G), dim3(NT), 0,
-                               c->stream, c->geo, L, dc, nullptr, nullptr, nullptr, c->rhs, x,
-                               c->r, c->st, c->partials, c->counter, rel_tol, abs_tol, max_iter,
-                               check_interval);
+        const double* rhs_in = (src == RHS_FROM_VELOCITY) ? nullptr : c->rhs;
+        if (src == RHS_FROM_VELOCITY) {
+            if (D)
+                hipLaunchKernelGGL((k_cg_setup<true, false, true, true>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
+                                   c->r, c->st, c->partials, c->counter, rel_tol, abs_tol,
+                                   max_iter, check_interval, c->dsum);
+            else
+                hipLaunchKernelGGL((k_cg_setup<true, false, true, false>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
+                                   c->r, c->st, c->partials, c->counter, rel_tol, abs_tol,
+                                   max_iter, check_interval, c->dsum);
+        } else {
+            if (D)
+                hipLaunchKernelGGL((k_cg_setup<false, false, true, true>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->geo, L, dc, nullptr, nullptr, nullptr,
+                                   (double*)rhs_in, x, c->r, c->st, c->partials, c->counter,
+                                   rel_tol, abs_tol, max_iter, check_interval, c->dsum);
+            else
+                hipLaunchKernelGGL((k_cg_setup<false, false, true, false>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->geo, L, dc, nullptr, nullptr, nullptr,
+                                   (double*)rhs_in, x, c->r, c->st, c->partials, c->counter,
+                                   rel_tol, abs_tol, max_iter, check_interval, c->dsum);
+        }
     });
+    if (D) {
+        ST_TRY(reduce_dot(c));
+        hipLaunchKernelGGL(k_finish_setup, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1,
+                           rel_tol, abs_tol, max_iter, check_interval);
+        ST_TRY(halo(c, {c->r}));
+    }
     double* P[2] = {c->pa, c->pb};
+    // one CG iteration: sweep A (+ all-reduce of (p,Ap), halo of the new p),
+    // sweep B (+ all-reduce of (r,r), halo of r)
+    auto iterate = [&](int it) -> cfd_status_t {
+        double* pnew = P[it & 1];
+        double* pold = P[(it + 1) & 1];
+        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, x, it); });
+        if (D) {
+            ST_TRY(reduce_dot(c));
+            hipLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1, it);
+            ST_TRY(halo(c, {pnew}));
+        }
+        timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); });
+        if (D) {
+            ST_TRY(reduce_dot(c));
+            hipLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1, it);
+            ST_TRY(halo(c, {c->r}));
+        }
+        return CFD_SUCCESS;
+    };
     int it = 0;
     if (max_iter > 0) {
-        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, true, L, c->r, P[1], P[0], x, 0); });
-        timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, P[0], c->r, 0); });
+        ST_TRY(iterate(0));
         it = 1;
     }
+    // Host polls a pinned copy of the device state once per chunk, one chunk
+    // behind (double-buffered), so the stream never drains while it waits.
+    // Every rank sees the same all-reduced state and leaves at the same chunk.
     int chunk = 8;
     const int chunk_max = std::max(1, c->cfg.poll_interval);
     int slot = 0, prev = -1;
     while (it < max_iter) {
         const int n = std::min(chunk, max_iter - it);
-        for (int q = 0; q < n; ++q, ++it) {
-            double* pnew = P[it & 1];
-            double* pold = P[(it + 1) & 1];
-            timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, false, L, c->r, pold, pnew, x, it); });
-            timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); });
-        }
+        for (int q = 0; q < n; ++q, ++it) ST_TRY(iterate(it));
         HIP_TRY(hipMemcpyAsync(&c->h_state[slot], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
                                c->stream));
         HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
@@ -302,6 +385,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     // final poisson_solver_apply_bc (cg.c:447); the breakdown exit skips it.
     if (final_bc && !stagnated && !(s.iterations == 0 && s.status == ST_CONVERGED))
         launch_bc(c, x, 0, dv);
+    ST_TRY(halo(c, {x}));
     c->pstats.status = (poisson_solver_status_t)s.status;
     c->pstats.iterations = s.iterations;
     c->pstats.initial_residual = s.res0;
@@ -330,8 +414,11 @@ static cfd_status_t residual_linf(hip_proj_ctx* c, const double* x, const ResCoe
         hipLaunchKernelGGL(k_residual_linf, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, x, c->rhs,
                            c->red + 4);
     });
-    HIP_TRY(hipMemcpyAsync(c->h_red, c->red, 8 * sizeof(unsigned long long),
-                           hipMemcpyDeviceToHost, c->stream));
+    cfd_status_t st;
+    const unsigned long long* red = reduce_red(c, &st);
+    if (st != CFD_SUCCESS) return st;
+    HIP_TRY(hipMemcpyAsync(c->h_red, red, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     *out = ord_dec(c->h_red[4]);
     return CFD_SUCCESS;
@@ -348,9 +435,10 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     rc.dy2 = dy * dy;
     rc.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
     rc.inv_factor = 1.0 / (2.0 * (1.0 / rc.dx2 + 1.0 / rc.dy2 + rc.inv_dz2));
-    rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nz, dx, dy, dz) : omega_in;
+    rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nzg, dx, dy, dz) : omega_in;
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
     const DirVals dv{};
+    ST_TRY(halo(c, {c->pn}));
     double res0 = 0.0;
     cfd_status_t s = residual_linf(c, c->pn, res_c, &res0);
     if (s != CFD_SUCCESS) return s;
@@ -372,6 +460,7 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
                 hipLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
                                    c->rhs, 1);
             });
+            ST_TRY(halo(c, {c->pn}));  // the black pass reads the neighbours' red cells
             timed(c, HIP_KT_RELAX, [&] {
                 hipLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
                                    c->rhs, 0);
@@ -385,6 +474,7 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
             // cells are rewritten by the Neumann gather)
             std::swap(c->pn, c->xt);
         }
+        ST_TRY(halo(c, {c->pn}));
         launch_bc(c, c->pn, 0, dv);
         if (iter % check_interval == 0) {
             s = residual_linf(c, c->pn, res_c, &res);
@@ -419,12 +509,12 @@ static cfd_status_t ensure_aux(hip_proj_ctx* c, bool need_rhs, bool need_xt) {
 static cfd_status_t validate_params(const hip_proj_ctx* c, const grid* g,
                                     const ns_solver_params_t* prm) {
     if (!g || !prm) return CFD_ERROR_INVALID;
-    if (g->nx != c->nx || g->ny != c->ny || g->nz != c->nz) {
+    if (g->nx != c->nx || g->ny != c->ny || g->nz != c->nzg) {
         set_err(CFD_ERROR_INVALID, "projection_hip: grid does not match the context");
         return CFD_ERROR_INVALID;
     }
-    if (c->nz > 1 && g->dz) {
-        for (size_t k = 1; k < c->nz - 1; k++)
+    if (g->nz > 1 && g->dz) {
+        for (size_t k = 1; k < g->nz - 1; k++)
             if (fabs(g->dz[k] - g->dz[0]) > 1e-14) {  // solver_projection.c:59-66
                 set_err(CFD_ERROR_INVALID, "projection_hip: non-uniform dz");
                 return CFD_ERROR_INVALID;
@@ -481,6 +571,8 @@ static void free_ctx(hip_proj_ctx* c) {
     if (c->partials) hipFree(c->partials);
     if (c->counter) hipFree(c->counter);
     if (c->red) hipFree(c->red);
+    if (c->redg) hipFree(c->redg);
+    if (c->dsum) hipFree(c->dsum);
     if (c->h_state) hipHostFree(c->h_state);
     if (c->h_red) hipHostFree(c->h_red);
     for (int i = 0; i < 2; i++)
@@ -510,6 +602,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     g.sz = (nz > 1) ? c->ps : 0;
     g.k0 = (nz > 1) ? 1 : 0;
     g.k1 = (nz > 1) ? (int)nz - 1 : 1;
+    g.lo_face = (c->rank == 0) ? 1 : 0;
+    g.hi_face = (c->rank == c->nranks - 1) ? 1 : 0;
+    g.kofs = (int)c->kofs;
     const int nint_k = g.k1 - g.k0;
     int kc = 0;
     if (kc <= 0) {
@@ -535,10 +630,20 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     sg.sz = g.sz;
     sg.k0 = g.k0;
     sg.k1 = g.k1;
-    sg.kc = (c->cfg.kchunk > 0) ? c->cfg.kchunk : 64;
-    sg.kc = std::max(1, std::min(sg.kc, nint_k));
     sg.tiles_x = (int)((nx + 127) / 128);
     sg.tiles_y = (int)((ny + c->sweep_ty - 1) / c->sweep_ty);
+    if (c->cfg.kchunk > 0) {
+        sg.kc = c->cfg.kchunk;
+    } else {
+        // 64-plane z runs, shortened (down to 16) until there are >= 4
+        // workgroups per CU: a thin slab must still fill all 256 CUs
+        sg.kc = 64;
+        const long long want = 4LL * c->grid_cap / 8;
+        while (sg.kc > 16 &&
+               (long long)sg.tiles_x * sg.tiles_y * ((nint_k + sg.kc - 1) / sg.kc) < want)
+            sg.kc /= 2;
+    }
+    sg.kc = std::max(1, std::min(sg.kc, nint_k));
     sg.tiles_z = (nint_k + sg.kc - 1) / sg.kc;
     const int n_partials = std::max(c->grid_cap, sg.tiles_x * sg.tiles_y * sg.tiles_z);
 
@@ -557,6 +662,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     HIP_TRY(hipMalloc((void**)&c->counter, 64));
     HIP_TRY(hipMemsetAsync(c->counter, 0, 64, c->stream));
     HIP_TRY(hipMalloc((void**)&c->red, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&c->redg, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&c->dsum, 4 * sizeof(double)));
+    HIP_TRY(hipMemsetAsync(c->dsum, 0, 4 * sizeof(double), c->stream));
     HIP_TRY(hipHostMalloc((void**)&c->h_state, 3 * sizeof(CgState), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&c->h_red, 8 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_poll[0], hipEventDisableTiming));
@@ -565,18 +673,17 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     return CFD_SUCCESS;
 }
 
-hip_proj_ctx_t* hip_proj_create(size_t nx, size_t ny, size_t nz, const hip_proj_config_t* cfg) {
-    if (nx < 3 || ny < 3 || nz == 0 || (nz > 1 && nz < 3)) {
-        set_err(CFD_ERROR_INVALID, "projection_hip: grid must be >= 3 points per active axis");
-        return nullptr;
-    }
+static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t nz_global,
+                                   SlabComm* comm, size_t kofs, const hip_proj_config_t* cfg) {
     if (!hip_projection_available()) {
         set_err(CFD_ERROR_UNSUPPORTED, "projection_hip: no HIP device available");
         return nullptr;
     }
     hip_proj_ctx* c = new hip_proj_ctx();
     c->cfg = cfg ? *cfg : hip_proj_config_default();
-    if (c->cfg.device < 0) {
+    if (comm) {
+        c->device = comm->device;
+    } else if (c->cfg.device < 0) {
         int d = 0;
         hipGetDevice(&d);
         c->device = d;
@@ -584,11 +691,64 @@ hip_proj_ctx_t* hip_proj_create(size_t nx, size_t ny, size_t nz, const hip_proj_
         c->device = c->cfg.device;
     }
     if (c->cfg.poll_interval <= 0) c->cfg.poll_interval = 64;
-    if (init_ctx(c, nx, ny, nz) != CFD_SUCCESS) {
+    c->comm = comm;
+    c->rank = comm ? comm->rank : 0;
+    c->nranks = comm ? comm->size : 1;
+    c->nzg = nz_global;
+    c->kofs = kofs;
+    if (init_ctx(c, nx, ny, nz_local) != CFD_SUCCESS) {
         free_ctx(c);
         return nullptr;
     }
     return c;
+}
+
+hip_proj_ctx_t* hip_proj_create(size_t nx, size_t ny, size_t nz, const hip_proj_config_t* cfg) {
+    if (nx < 3 || ny < 3 || nz == 0 || (nz > 1 && nz < 3)) {
+        set_err(CFD_ERROR_INVALID, "projection_hip: grid must be >= 3 points per active axis");
+        return nullptr;
+    }
+    return create_common(nx, ny, nz, nz, nullptr, 0, cfg);
+}
+
+cfd_status_t hip_proj_slab_layout(size_t nz, int rank, int size, size_t* k_offset,
+                                  size_t* nz_local) {
+    if (nz < 3 || size < 1 || rank < 0 || rank >= size || (size_t)size > nz - 2)
+        return CFD_ERROR_INVALID;
+    // interior planes 1..nz-2 split as evenly as possible, lower ranks first
+    const size_t nint = nz - 2, base = nint / (size_t)size, rem = nint % (size_t)size;
+    const size_t r = (size_t)rank;
+    const size_t first = 1 + r * base + std::min(r, rem);
+    const size_t count = base + (r < rem ? 1 : 0);
+    if (k_offset) *k_offset = first - 1;
+    if (nz_local) *nz_local = count + 2;
+    return CFD_SUCCESS;
+}
+
+hip_proj_ctx_t* hip_proj_create_slab(size_t nx, size_t ny, size_t nz, hip_proj_comm_t* comm,
+                                     const hip_proj_config_t* cfg) {
+    if (!comm || !comm->impl) {
+        set_err(CFD_ERROR_INVALID, "hip_proj_create_slab: no communicator");
+        return nullptr;
+    }
+    size_t kofs = 0, nzl = 0;
+    if (nx < 3 || ny < 3 ||
+        hip_proj_slab_layout(nz, comm->impl->rank, comm->impl->size, &kofs, &nzl) != CFD_SUCCESS) {
+        set_err(CFD_ERROR_INVALID,
+                "hip_proj_create_slab: 3-D grid with at least one interior plane per rank needed");
+        return nullptr;
+    }
+    return create_common(nx, ny, nzl, nz, comm->impl, kofs, cfg);
+}
+
+cfd_status_t hip_proj_slab_info(const hip_proj_ctx_t* c, size_t* k_offset, size_t* nz_local,
+                                int* rank, int* size) {
+    if (!c) return CFD_ERROR_INVALID;
+    if (k_offset) *k_offset = c->kofs;
+    if (nz_local) *nz_local = c->nz;
+    if (rank) *rank = c->rank;
+    if (size) *size = c->nranks;
+    return CFD_SUCCESS;
 }
 
 void hip_proj_destroy(hip_proj_ctx_t* ctx) { free_ctx(ctx); }
@@ -703,6 +863,16 @@ cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type)
         return CFD_ERROR_UNSUPPORTED;
     }
     HIP_TRY(hipSetDevice(c->device));
+    if (mode == 1 && dist(c)) {
+        // periodic z across slabs: x/y ring on every local plane, then the
+        // z copy (plane 0 <- nz-2, nz-1 <- 1) as a wrap-around halo exchange
+        Geo g = c->geo;
+        g.lo_face = g.hi_face = 0;
+        hipLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, g, d, mode,
+                           DirVals{});
+        HIP_TRY(hipGetLastError());
+        return halo(c, {d}, true);
+    }
     launch_bc(c, d, mode, DirVals{});
     HIP_TRY(hipGetLastError());
     return CFD_SUCCESS;
@@ -756,7 +926,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     cfd_status_t s = validate_params(c, g, prm);
     if (s != CFD_SUCCESS) return s;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t nx = c->nx, ny = c->ny, nz = c->nz;
+    const size_t nx = c->nx, ny = c->ny, nz = c->nzg;
     const double dx = g->dx[0], dy = g->dy[0];
     const double dz = (nz > 1 && g->dz) ? g->dz[0] : 0.0;
     const double dt = prm->dt;
@@ -795,6 +965,9 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     pc.g1 = prm->gravity[1];
     pc.g2 = prm->gravity[2];
     const dim3 cg = cell_grid(c);
+    // slabs: the neighbours' planes of everything the stencils read
+    ST_TRY(halo(c, {c->u, c->v, c->w, c->p}));
+    if (buoy) ST_TRY(halo(c, {c->T}));
     timed(c, HIP_KT_PREDICTOR, [&] {
         if (buoy)
             hipLaunchKernelGGL(k_predictor<true>, cg, dim3(256), 0, c->stream, c->geo, pc, c->u,
@@ -804,6 +977,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
     });
     HIP_TRY(hipGetLastError());
+    ST_TRY(halo(c, {c->ws}));  // d(w*)/dz of the divergence
 
     // p_new = p (solver_projection.c:108)
     HIP_TRY(hipMemcpyAsync(c->pn, c->p, field_elems(c) * sizeof(double), hipMemcpyDeviceToDevice,
@@ -830,7 +1004,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
         const int G = tile_grid(c);
         hipLaunchKernelGGL((k_cg_setup<true, true, false>), dim3(G), dim3(NT), 0, c->stream,
                            c->geo, L, dc, c->us, c->vs, c->ws, c->rhs, c->pn, c->r, c->st,
-                           c->partials, c->counter, 0.0, 0.0, 0, 1);
+                           c->partials, c->counter, 0.0, 0.0, 0, 1, c->dsum);
         if (method == HIP_POISSON_JACOBI)
             HIP_TRY(hipMemsetAsync(c->xt, 0, field_elems(c) * sizeof(double), c->stream));
         int maxit = c->cfg.poisson_max_iter;
@@ -850,12 +1024,17 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     cc.dt_over_rho = dt / rho;
     hipLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->red);
     timed(c, HIP_KT_CORRECTOR, [&] {
-        hipLaunchKernelGGL(k_corrector, cg, dim3(256), 0, c->stream, c->geo, cc, c->us, c->vs,
+        const int ks = (c->nz > 1 && !c->geo.lo_face) ? 1 : 0;
+        const int ke = (c->nz > 1 && !c->geo.hi_face) ? (int)c->nz - 1 : (int)c->nz;
+        const dim3 cgz(cg.x, cg.y, (unsigned)((ke - ks + CORR_KC - 1) / CORR_KC));
+        hipLaunchKernelGGL(k_corrector, cgz, dim3(256), 0, c->stream, c->geo, cc, c->us, c->vs,
                            c->ws, c->pn, c->u, c->v, c->w, c->red);
     });
     std::swap(c->p, c->pn);  // memcpy(field->p, p_new) (solver_projection.c:253)
-    HIP_TRY(hipMemcpyAsync(c->h_red, c->red, 8 * sizeof(unsigned long long),
-                           hipMemcpyDeviceToHost, c->stream));
+    const unsigned long long* red = reduce_red(c, &s);
+    if (s != CFD_SUCCESS) return s;
+    HIP_TRY(hipMemcpyAsync(c->h_red, red, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     flush_timing(c);
     if (c->h_red[2]) {
@@ -919,7 +1098,7 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter
 extern "C" __attribute__((visibility("hidden"))) int hip_proj_matches_internal(const hip_proj_ctx_t* c,
                                                                     size_t nx, size_t ny,
                                                                     size_t nz) {
-    return c && c->nx == nx && c->ny == ny && c->nz == nz;
+    return c && c->nranks == 1 && c->nx == nx && c->ny == ny && c->nzg == nz;
 }
 
 extern "C" {

@@ -1,0 +1,330 @@
+// slab_comm.hip -- RCCL and in-process backends of SlabComm (slab_comm.hpp)
+// and their C-ABI constructors (include/cfd_hip/projection_hip.h).
+#include "slab_comm.hpp"
+
+#include "cfd_hip/projection_hip.h"
+
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+extern "C" void cfd_set_error(cfd_status_t status, const char* message) __attribute__((weak));
+
+static cfd_status_t fail(cfd_status_t s, const char* what, const char* detail) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "slab comm: %s%s%s", what, detail ? ": " : "", detail ? detail : "");
+    if (cfd_set_error) cfd_set_error(s, buf);
+    return s;
+}
+
+#define HIPC(call)                                                                  \
+    do {                                                                            \
+        hipError_t e_ = (call);                                                     \
+        if (e_ != hipSuccess) return fail(CFD_ERROR, #call, hipGetErrorString(e_)); \
+    } while (0)
+
+#define NCCLC(call)                                                                    \
+    do {                                                                               \
+        ncclResult_t r_ = (call);                                                      \
+        if (r_ != ncclSuccess) return fail(CFD_ERROR, #call, ncclGetErrorString(r_));  \
+    } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// RCCL: halo planes move with grouped ncclSend/ncclRecv (one plane each way
+// per neighbour and field, point-to-point over xGMI), dot products with an
+// 8-B ncclAllReduce. Everything is stream-ordered on the caller's stream.
+// ---------------------------------------------------------------------------
+struct RcclComm final : SlabComm {
+    ncclComm_t comm = nullptr;
+    ~RcclComm() override {
+        if (comm) ncclCommDestroy(comm);
+    }
+    // Posting order matters only when both neighbours are the same peer
+    // (2 ranks, periodic): sends go to-lower then to-upper, receives come
+    // from-upper then from-lower, so the k-th send to a peer always pairs
+    // with the k-th receive the peer posts from us.
+    cfd_status_t halo(hipStream_t s, double* const* f, int nf, long long ps, int nz,
+                      bool periodic) override {
+        if (size == 1) return CFD_SUCCESS;
+        const int lo = lower(periodic), hi = upper(periodic);
+        NCCLC(ncclGroupStart());
+        for (int q = 0; q < nf; ++q) {
+            if (lo >= 0) NCCLC(ncclSend(f[q] + ps, (size_t)ps, ncclDouble, lo, comm, s));
+            if (hi >= 0) NCCLC(ncclSend(f[q] + ps * (nz - 2), (size_t)ps, ncclDouble, hi, comm, s));
+            if (hi >= 0) NCCLC(ncclRecv(f[q] + ps * (nz - 1), (size_t)ps, ncclDouble, hi, comm, s));
+            if (lo >= 0) NCCLC(ncclRecv(f[q], (size_t)ps, ncclDouble, lo, comm, s));
+        }
+        NCCLC(ncclGroupEnd());
+        return CFD_SUCCESS;
+    }
+    cfd_status_t allreduce_sum(hipStream_t s, const double* in, double* out, int n) override {
+        NCCLC(ncclAllReduce(in, out, (size_t)n, ncclDouble, ncclSum, comm, s));
+        return CFD_SUCCESS;
+    }
+    cfd_status_t allreduce_max_u64(hipStream_t s, const unsigned long long* in,
+                                   unsigned long long* out, int n) override {
+        NCCLC(ncclAllReduce(in, out, (size_t)n, ncclUint64, ncclMax, comm, s));
+        return CFD_SUCCESS;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// In-process group: each rank's host thread publishes what it exposes,
+// records an event, meets the others at a host barrier, makes its stream wait
+// on the peers' events, pulls / reduces, records a second event and meets
+// them again so no rank reuses a buffer a peer is still reading.
+// ---------------------------------------------------------------------------
+constexpr int GROUP_MAX = 16;
+struct GroupPtrs {
+    const void* p[GROUP_MAX];
+    int n;
+};
+
+__global__ void k_group_sum(GroupPtrs in, double* out, int count) {
+    for (int e = threadIdx.x; e < count; e += blockDim.x) {
+        double s = 0.0;
+        for (int r = 0; r < in.n; ++r) s += ((const double*)in.p[r])[e];  // rank order
+        out[e] = s;
+    }
+}
+
+__global__ void k_group_max_u64(GroupPtrs in, unsigned long long* out, int count) {
+    for (int e = threadIdx.x; e < count; e += blockDim.x) {
+        unsigned long long m = 0;
+        for (int r = 0; r < in.n; ++r) {
+            const unsigned long long v = ((const unsigned long long*)in.p[r])[e];
+            m = v > m ? v : m;
+        }
+        out[e] = m;
+    }
+}
+
+}  // namespace
+
+struct hip_proj_group {
+    int size = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    unsigned long long gen = 0;
+    bool broken = false;
+    int timeout_s = 300;
+    std::vector<hipEvent_t> ev_ready, ev_done;
+    std::vector<const void*> pub;
+    std::vector<double* const*> pubf;
+    std::vector<int> pubnz, joined;
+
+    // false once any rank timed out: a rank that failed before reaching a
+    // collective must not leave the others blocked forever.
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (broken) return false;
+        const unsigned long long my = gen;
+        if (++arrived == size) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::seconds(timeout_s),
+                                    [&] { return gen != my || broken; });
+        if (!ok || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+
+namespace {
+
+struct LocalComm final : SlabComm {
+    hip_proj_group* G = nullptr;
+
+    cfd_status_t meet() {
+        if (!G->barrier()) return fail(CFD_ERROR, "in-process group barrier timed out", nullptr);
+        return CFD_SUCCESS;
+    }
+    cfd_status_t wait_all(hipStream_t s, const std::vector<hipEvent_t>& ev) {
+        for (int r = 0; r < size; ++r)
+            if (r != rank) HIPC(hipStreamWaitEvent(s, ev[r], 0));
+        return CFD_SUCCESS;
+    }
+    cfd_status_t halo(hipStream_t s, double* const* f, int nf, long long ps, int nz,
+                      bool periodic) override {
+        if (size == 1) return CFD_SUCCESS;
+        const int lo = lower(periodic), hi = upper(periodic);
+        G->pubf[rank] = f;
+        G->pubnz[rank] = nz;
+        HIPC(hipEventRecord(G->ev_ready[rank], s));
+        cfd_status_t st = meet();
+        if (st != CFD_SUCCESS) return st;
+        if (lo >= 0) HIPC(hipStreamWaitEvent(s, G->ev_ready[lo], 0));
+        if (hi >= 0 && hi != lo) HIPC(hipStreamWaitEvent(s, G->ev_ready[hi], 0));
+        const size_t bytes = (size_t)ps * sizeof(double);
+        for (int q = 0; q < nf; ++q) {
+            if (lo >= 0) {
+                const double* src = G->pubf[lo][q] + ps * (G->pubnz[lo] - 2);
+                HIPC(hipMemcpyAsync(f[q], src, bytes, hipMemcpyDeviceToDevice, s));
+            }
+            if (hi >= 0) {
+                const double* src = G->pubf[hi][q] + ps;
+                HIPC(hipMemcpyAsync(f[q] + ps * (nz - 1), src, bytes, hipMemcpyDeviceToDevice, s));
+            }
+        }
+        HIPC(hipEventRecord(G->ev_done[rank], s));
+        if ((st = meet()) != CFD_SUCCESS) return st;
+        // peers pulled from our owned planes; do not overwrite them before that
+        if (lo >= 0) HIPC(hipStreamWaitEvent(s, G->ev_done[lo], 0));
+        if (hi >= 0 && hi != lo) HIPC(hipStreamWaitEvent(s, G->ev_done[hi], 0));
+        return CFD_SUCCESS;
+    }
+    template <typename K>
+    cfd_status_t reduce(hipStream_t s, const void* in, K launch) {
+        G->pub[rank] = in;
+        HIPC(hipEventRecord(G->ev_ready[rank], s));
+        cfd_status_t st = meet();
+        if (st != CFD_SUCCESS) return st;
+        if ((st = wait_all(s, G->ev_ready)) != CFD_SUCCESS) return st;
+        GroupPtrs ptrs{};
+        ptrs.n = size;
+        for (int r = 0; r < size; ++r) ptrs.p[r] = G->pub[r];
+        launch(ptrs);
+        HIPC(hipGetLastError());
+        HIPC(hipEventRecord(G->ev_done[rank], s));
+        if ((st = meet()) != CFD_SUCCESS) return st;
+        return wait_all(s, G->ev_done);
+    }
+    cfd_status_t allreduce_sum(hipStream_t s, const double* in, double* out, int n) override {
+        return reduce(s, in, [&](const GroupPtrs& p) {
+            hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, s, p, out, n);
+        });
+    }
+    cfd_status_t allreduce_max_u64(hipStream_t s, const unsigned long long* in,
+                                   unsigned long long* out, int n) override {
+        return reduce(s, in, [&](const GroupPtrs& p) {
+            hipLaunchKernelGGL(k_group_max_u64, dim3(1), dim3(64), 0, s, p, out, n);
+        });
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+cfd_status_t hip_proj_comm_unique_id(unsigned char id[HIP_PROJ_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == HIP_PROJ_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    if (!id) return CFD_ERROR_INVALID;
+    ncclUniqueId u;
+    NCCLC(ncclGetUniqueId(&u));
+    memcpy(id, &u, sizeof(u));
+    return CFD_SUCCESS;
+}
+
+hip_proj_comm_t* hip_proj_comm_create_rccl(const unsigned char id[HIP_PROJ_UNIQUE_ID_BYTES],
+                                           int rank, int size, int device) {
+    if (!id || size < 1 || rank < 0 || rank >= size) {
+        fail(CFD_ERROR_INVALID, "bad rank/size", nullptr);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        fail(CFD_ERROR, "hipSetDevice failed", nullptr);
+        return nullptr;
+    }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    auto* c = new RcclComm();
+    c->rank = rank;
+    c->size = size;
+    c->device = device;
+    ncclResult_t r = ncclCommInitRank(&c->comm, size, u, rank);
+    if (r != ncclSuccess) {
+        fail(CFD_ERROR, "ncclCommInitRank", ncclGetErrorString(r));
+        c->comm = nullptr;
+        delete c;
+        return nullptr;
+    }
+    auto* h = new hip_proj_comm();
+    h->impl = c;
+    return h;
+}
+
+hip_proj_group_t* hip_proj_group_create(int size) {
+    if (size < 1 || size > GROUP_MAX) {
+        fail(CFD_ERROR_INVALID, "group size must be 1..16", nullptr);
+        return nullptr;
+    }
+    auto* g = new hip_proj_group();
+    g->size = size;
+    if (const char* t = getenv("CFD_HIP_GROUP_TIMEOUT_S")) g->timeout_s = std::max(1, atoi(t));
+    g->ev_ready.assign(size, nullptr);
+    g->ev_done.assign(size, nullptr);
+    g->pub.assign(size, nullptr);
+    g->pubf.assign(size, nullptr);
+    g->pubnz.assign(size, 0);
+    g->joined.assign(size, 0);
+    return g;
+}
+
+void hip_proj_group_destroy(hip_proj_group_t* g) {
+    if (!g) return;
+    for (auto e : g->ev_ready)
+        if (e) hipEventDestroy(e);
+    for (auto e : g->ev_done)
+        if (e) hipEventDestroy(e);
+    delete g;
+}
+
+hip_proj_comm_t* hip_proj_comm_create_local(hip_proj_group_t* g, int rank, int device) {
+    if (!g || rank < 0 || rank >= g->size || g->joined[rank]) {
+        fail(CFD_ERROR_INVALID, "bad group rank", nullptr);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_ready[rank], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_done[rank], hipEventDisableTiming) != hipSuccess) {
+        fail(CFD_ERROR, "event creation failed", nullptr);
+        return nullptr;
+    }
+    // ranks on other devices read this one's buffers directly (best effort;
+    // fails harmlessly when already enabled or on the same device)
+    int ndev = 0;
+    hipGetDeviceCount(&ndev);
+    for (int d = 0; d < ndev; ++d) {
+        int ok = 0;
+        if (d != device && hipDeviceCanAccessPeer(&ok, device, d) == hipSuccess && ok) {
+            hipDeviceEnablePeerAccess(d, 0);
+            (void)hipGetLastError();
+        }
+    }
+    g->joined[rank] = 1;
+    auto* c = new LocalComm();
+    c->G = g;
+    c->rank = rank;
+    c->size = g->size;
+    c->device = device;
+    auto* h = new hip_proj_comm();
+    h->impl = c;
+    return h;
+}
+
+void hip_proj_comm_destroy(hip_proj_comm_t* c) {
+    if (!c) return;
+    delete c->impl;
+    delete c;
+}
+
+int hip_proj_comm_rank(const hip_proj_comm_t* c) { return c && c->impl ? c->impl->rank : -1; }
+int hip_proj_comm_size(const hip_proj_comm_t* c) { return c && c->impl ? c->impl->size : 0; }
+
+}  // extern "C"

@@ -158,6 +158,48 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* ctx, int meth
                                                    const poisson_solver_params_t* params,
                                                    poisson_solver_stats_t* stats);
 
+/* ---- Z-slab multi-GPU ------------------------------------------------------
+ * The reference runs one device per simulation (solver_projection_gpu.cu has
+ * no decomposition). Here the nz-2 interior planes of the
+ * global grid are split into contiguous slabs, one per rank: rank r holds
+ * nz_local = owned + 2 planes, local plane 0 being global plane k_offset.
+ * The two outer local planes are the global z faces on the edge ranks and
+ * halo copies of the neighbours' planes elsewhere. Every CG dot product is a
+ * per-rank deterministic partial summed by an all-reduce; the textbook CG
+ * iteration otherwise keeps its single-device semantics. Fields passed to
+ * set_field/get_field/poisson_solve are the rank's nx*ny*nz_local slab; the
+ * grid passed to step functions is the GLOBAL grid.
+ *
+ * Communicators: RCCL (one process per GPU; rank 0 creates the unique id, the
+ * caller broadcasts its bytes, e.g. over torch.distributed) or an in-process
+ * group whose ranks are slab contexts of one process, each driven from its
+ * own host thread (all ranks call every step function concurrently). */
+#define HIP_PROJ_UNIQUE_ID_BYTES 128
+typedef struct hip_proj_comm hip_proj_comm_t;
+typedef struct hip_proj_group hip_proj_group_t;
+
+/* Split of nz (global points) for `rank` of `size`; host-only, no device. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_slab_layout(size_t nz, int rank, int size, size_t* k_offset,
+                                                 size_t* nz_local);
+CFD_HIP_EXPORT cfd_status_t hip_proj_comm_unique_id(unsigned char id[HIP_PROJ_UNIQUE_ID_BYTES]);
+/* Collective over the `size` processes (ncclCommInitRank on `device`). */
+CFD_HIP_EXPORT hip_proj_comm_t* hip_proj_comm_create_rccl(
+    const unsigned char id[HIP_PROJ_UNIQUE_ID_BYTES], int rank, int size, int device);
+CFD_HIP_EXPORT hip_proj_group_t* hip_proj_group_create(int size);
+CFD_HIP_EXPORT void hip_proj_group_destroy(hip_proj_group_t* group);
+CFD_HIP_EXPORT hip_proj_comm_t* hip_proj_comm_create_local(hip_proj_group_t* group, int rank,
+                                                           int device);
+CFD_HIP_EXPORT void hip_proj_comm_destroy(hip_proj_comm_t* comm);
+CFD_HIP_EXPORT int hip_proj_comm_rank(const hip_proj_comm_t* comm);
+CFD_HIP_EXPORT int hip_proj_comm_size(const hip_proj_comm_t* comm);
+/* Slab context for rank comm_rank of the global nx*ny*nz grid (3-D only). The
+ * communicator must outlive the context. */
+CFD_HIP_EXPORT hip_proj_ctx_t* hip_proj_create_slab(size_t nx, size_t ny, size_t nz,
+                                                    hip_proj_comm_t* comm,
+                                                    const hip_proj_config_t* cfg);
+CFD_HIP_EXPORT cfd_status_t hip_proj_slab_info(const hip_proj_ctx_t* ctx, size_t* k_offset,
+                                               size_t* nz_local, int* rank, int* size);
+
 /* ---- plugin surface ------------------------------------------------------ */
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_rbsor_solver(void);

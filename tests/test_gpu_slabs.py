@@ -1,0 +1,245 @@
+"""Z-slab decomposition on the GPU, run as an in-process group
+of slab contexts on one device: the same driver code, halo exchanges and
+all-reduces the RCCL backend runs one process per GPU, with the transport
+replaced by device copies (RCCL refuses two ranks on one GPU).
+
+Parity bars: the relaxation methods have no summation, so a slab run is
+bitwise the single-domain oracle; CG dot products are summed per slab and
+then across slabs, so CG runs agree to rounding (same bar as the 1-GPU CG)."""
+import numpy as np
+import pytest
+
+from cfd_amd import _abi as A
+from cfd_amd import api
+from oracle import oracle
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = {"u": A.HIP_FIELD_U, "v": A.HIP_FIELD_V, "w": A.HIP_FIELD_W, "p": A.HIP_FIELD_P}
+
+
+@pytest.fixture(autouse=True)
+def _short_group_timeout(monkeypatch):
+    monkeypatch.setenv("CFD_HIP_GROUP_TIMEOUT_S", "60")
+
+
+class Slabs:
+    def __init__(self, g, nranks, **cfg):
+        self.g = g
+        self.group = api.LocalGroup(nranks)
+        self.ctx = [api.HipProjection(g.nx, g.ny, g.nz, comm=self.group.comm(r, 0), **cfg)
+                    for r in range(nranks)]
+        self.n = nranks
+
+    def scatter(self, f):
+        for c in self.ctx:
+            sl = slice(c.k_offset, c.k_offset + c.nz_local)
+            for k, fid in FIELDS.items():
+                c.set_field(fid, getattr(f, k)[sl])
+            c.set_density(float(f.rho.flat[0]))
+
+    def gather(self, name):
+        out = np.full((self.g.nz, self.g.ny, self.g.nx), np.nan)
+        for c in self.ctx:
+            loc, glob = c.owned()
+            out[glob] = c.get_field(FIELDS[name])[loc]
+        assert not np.isnan(out).any()
+        return out
+
+    def run(self, fn):
+        return api.run_ranks(lambda r: fn(r, self.ctx[r]), self.n)
+
+    def close(self):
+        for c in self.ctx:
+            c.close()
+        self.group.close()
+
+
+def _cavity_bc_device(c):
+    c.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
+    c.apply_dirichlet(A.HIP_FIELD_V, api.dirichlet())
+    c.apply_dirichlet(A.HIP_FIELD_W, api.dirichlet())
+    c.apply_scalar_bc(A.HIP_FIELD_P, A.BC_TYPE_NEUMANN)
+
+
+def _tg_bc_device(c):
+    for fid in FIELDS.values():
+        c.apply_scalar_bc(fid, A.BC_TYPE_PERIODIC)
+
+
+def _run_steps(S, g, p, n_steps, bc_dev):
+    def body(r, c):
+        out = []
+        for _ in range(n_steps):
+            bc_dev(c)
+            st = A.SolverStats()
+            s = c.step_device(g, p, st)
+            assert s == A.CFD_SUCCESS, (r, s, api._native.last_error())
+            out.append((c.poisson_stats().iterations, st.max_velocity, st.max_pressure))
+        return out
+    return S.run(body)
+
+
+def _oracle_steps(g, f, p, n_steps, bc_host, kind):
+    hist = []
+    for _ in range(n_steps):
+        bc_host(f)
+        s, st, it = oracle.projection_step(f, g, p, kind)
+        assert s == A.CFD_SUCCESS
+        hist.append((it, st.max_velocity, st.max_pressure))
+    return hist
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_slab_layout_covers_interior(hip_lib, nranks):
+    nz = 17
+    spans = [api.slab_layout(nz, r, nranks) for r in range(nranks)]
+    owned = []
+    for ko, nl in spans:
+        owned += list(range(ko + 1, ko + nl - 1))
+    assert owned == list(range(1, nz - 1))
+    assert max(nl for _, nl in spans) - min(nl for _, nl in spans) <= 1
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("bc", ["neumann", "periodic"])
+def test_slab_scalar_bc_bitwise(hip_lib, nranks, bc):
+    """Device BCs on slabs (z faces on the edge ranks; periodic z as the
+    wrap-around exchange) equal the reference's host BC on the whole field."""
+    nx, ny, nz = 17, 13, 11
+    rng = np.random.default_rng(11)
+    ref = rng.standard_normal((nz, ny, nx))
+    g = api.Grid(nx, ny, nz, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
+    f = api.FlowField(nx, ny, nz)
+    f.p[...] = ref
+    f.u[...] = f.v[...] = f.w[...] = 0.0
+    f.rho[...] = 1.0
+    S = Slabs(g, nranks)
+    try:
+        S.scatter(f)
+        t = A.BC_TYPE_NEUMANN if bc == "neumann" else A.BC_TYPE_PERIODIC
+        S.run(lambda r, c: c.apply_scalar_bc(A.HIP_FIELD_P, t))
+        got = S.gather("p")
+    finally:
+        S.close()
+    want = ref.copy()
+    api.bc_apply_scalar_3d(want, t)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("method,nranks", [(A.HIP_POISSON_REDBLACK, 2),
+                                           (A.HIP_POISSON_REDBLACK, 4),
+                                           (A.HIP_POISSON_JACOBI, 3)])
+def test_slab_relaxation_projection_bitwise(hip_lib, method, nranks):
+    """RB-SOR (global colour parity, halo after each colour) and Jacobi on
+    slabs: bitwise the single-domain oracle, iteration counts included."""
+    g, f, p = cases.cavity(17, 17, 17, Re=100.0, dt=5e-4)
+    maxit = 2000 if method == A.HIP_POISSON_JACOBI else 5000
+    okind = (A.ORACLE_POISSON_REDBLACK if method == A.HIP_POISSON_REDBLACK
+             else A.ORACLE_POISSON_JACOBI)
+    S = Slabs(g, nranks, poisson_method=method, poisson_tolerance=1e-2, poisson_max_iter=maxit)
+    try:
+        S.scatter(f)
+        hist = _run_steps(S, g, p, 3, _cavity_bc_device)
+        got = {k: S.gather(k) for k in FIELDS}
+    finally:
+        S.close()
+    oracle.set_projection_poisson_params(
+        oracle.poisson_params(tolerance=1e-2, max_iterations=maxit))
+    try:
+        ohist = _oracle_steps(g, f, p, 3, lambda ff: api.cavity_bc(ff, 1.0), okind)
+    finally:
+        oracle.set_projection_poisson_params(None)
+    for r in range(nranks):
+        assert hist[r] == ohist, (r, hist[r], ohist)
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], getattr(f, k), err_msg=k)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_slab_cg_cavity_vs_oracle(hip_lib, nranks):
+    g, f, p = cases.cavity(33, 33, 33, Re=100.0, dt=5e-4)
+    S = Slabs(g, nranks)
+    try:
+        S.scatter(f)
+        hist = _run_steps(S, g, p, 4, _cavity_bc_device)
+        got = {k: S.gather(k) for k in FIELDS}
+    finally:
+        S.close()
+    ohist = _oracle_steps(g, f, p, 4, lambda ff: api.cavity_bc(ff, 1.0), A.ORACLE_POISSON_CG)
+    for r in range(nranks):
+        assert hist[r] == hist[0]  # every rank holds the same all-reduced state
+    for (ih, vh, ph), (io, vo, po) in zip(hist[0], ohist):
+        assert abs(ih - io) <= 1
+        assert vh == pytest.approx(vo, rel=1e-9)
+        assert ph == pytest.approx(po, rel=1e-9)
+    for k in FIELDS:
+        ref = getattr(f, k)
+        scale = max(1.0, float(np.max(np.abs(ref))))
+        assert float(np.max(np.abs(got[k] - ref))) / scale <= 1e-10, k
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_slab_taylor_green_vs_oracle(hip_lib, nranks):
+    """Config 4 at test size: periodic BCs across the slab boundary every step
+    (with 2 ranks both neighbours of each rank are the same peer)."""
+    g, f, p = cases.tg3(17)
+    S = Slabs(g, nranks)
+    try:
+        S.scatter(f)
+        _run_steps(S, g, p, 5, _tg_bc_device)
+        got = {k: S.gather(k) for k in FIELDS}
+    finally:
+        S.close()
+    _oracle_steps(g, f, p, 5, cases.tg3_bc, A.ORACLE_POISSON_CG)
+    for k in FIELDS:
+        ref = getattr(f, k)
+        scale = max(1.0, float(np.max(np.abs(ref))))
+        assert float(np.max(np.abs(got[k] - ref))) / scale <= 1e-10, k
+
+
+def _slab_poisson(g, rhs, nranks, method, prm=None):
+    S = Slabs(g, nranks)
+    try:
+        def body(r, c):
+            sl = slice(c.k_offset, c.k_offset + c.nz_local)
+            x = np.zeros(c.shape)
+            s, st = c.poisson_solve(method, x, rhs[sl], g.dx, g.dy, g.dz, prm)
+            return s, st.iterations, x
+        res = S.run(body)
+        x = np.full(rhs.shape, np.nan)
+        for c, (s, it, xl) in zip(S.ctx, res):
+            loc, glob = c.owned()
+            x[glob] = xl[loc]
+    finally:
+        S.close()
+    assert not np.isnan(x).any()
+    return [r[0] for r in res], [r[1] for r in res], x
+
+
+def test_slab_poisson_cg_vs_oracle(hip_lib):
+    """Standalone slab CG: the reference's iteration count and demeaned gate."""
+    g, rhs = cases.cos_rhs(33)
+    xo = np.zeros_like(rhs)
+    so, sto = oracle.cg_solve(xo, rhs, g.dx, g.dy, g.dz)
+    stat, its, x = _slab_poisson(g, rhs, 3, A.HIP_POISSON_CG)
+    assert so == A.CFD_SUCCESS and all(s == A.CFD_SUCCESS for s in stat)
+    assert len(set(its)) == 1 and abs(its[0] - sto.iterations) <= 1
+    d = (x - x.mean()) - (xo - xo.mean())
+    assert np.max(np.abs(d)) / np.max(np.abs(xo)) < 1e-9
+
+
+@pytest.mark.parametrize("method", [A.HIP_POISSON_REDBLACK, A.HIP_POISSON_JACOBI])
+def test_slab_poisson_relax_bitwise(hip_lib, method):
+    g, rhs = cases.cos_rhs(17)
+    xo = np.zeros_like(rhs)
+    prm = oracle.poisson_params(max_iterations=3000 if method == A.HIP_POISSON_JACOBI else 5000)
+    if method == A.HIP_POISSON_REDBLACK:
+        so, sto = oracle.redblack_solve(xo, rhs, g.dx, g.dy, g.dz, prm)
+    else:
+        so, sto = oracle.jacobi_solve(xo, rhs, g.dx, g.dy, g.dz, prm)
+    stat, its, x = _slab_poisson(g, rhs, 4, method, prm)
+    assert all(s == so for s in stat)
+    assert all(i == sto.iterations for i in its)
+    np.testing.assert_array_equal(x, xo)
