@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--dt", type=float, default=1e-4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-cg-iters", type=int, default=10,
+    ap.add_argument("--cpu-cg-iters", type=int, default=100,
                     help="CG iterations timed in the CPU baseline sample")
     ap.add_argument("--kchunk", type=int, default=0)
     ap.add_argument("--sweep-rows", type=int, default=8)
