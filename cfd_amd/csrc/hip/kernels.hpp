@@ -444,6 +444,15 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
     double2 pc = xok ? (FIRST ? ld2(r, idx) : make_double2(ld2(r, idx).x + beta * oc.x,
                                                           ld2(r, idx).y + beta * oc.y)) : zero;
     double2 hc = (xok && halo) ? PV(idx + hoff) : zero;
+    // Z-slabs: p is pointwise in r and p_old, so the tiles at the slab ends
+    // also write the new p on the halo planes (r's halo is exchanged after
+    // sweep B); sweep B then needs no halo exchange of p.
+    if (DIST && c.act && c.kb == g.k0) {
+        double2 pw;
+        pw.x = c.in0 ? pm.x : 0.0;
+        pw.y = c.in1 ? pm.y : 0.0;
+        st2(pn, idx - g.sz, pw);
+    }
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
         const long long ip = idx + g.sz;
@@ -484,6 +493,12 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
         oc = op;
         hc = hp;
         buf ^= 1;
+    }
+    if (DIST && c.act && c.ke == g.k1) {  // pc = p on plane k1 (upper halo)
+        double2 pw;
+        pw.x = c.in0 ? pc.x : 0.0;
+        pw.y = c.in1 ? pc.y : 0.0;
+        st2(pn, idx, pw);
     }
 #undef PV
 #undef PS

@@ -72,6 +72,8 @@ struct hip_proj_ctx {
     size_t nzg = 0;    // global nz
     size_t kofs = 0;   // global index of local plane 0
     double* dsum = nullptr;            // [0] local dot total, [1] all-reduced
+    hipStream_t hstream = nullptr;     // side stream: halo of r overlaps the (r,r) all-reduce
+    hipEvent_t ev_b = nullptr, ev_h = nullptr;
     unsigned long long* redg = nullptr;  // all-reduced red[]
     // fields
     double *u = nullptr, *v = nullptr, *w = nullptr, *p = nullptr, *T = nullptr;
@@ -330,8 +332,8 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         ST_TRY(halo(c, {c->r}));
     }
     double* P[2] = {c->pa, c->pb};
-    // one CG iteration: sweep A (+ all-reduce of (p,Ap), halo of the new p),
-    // sweep B (+ all-reduce of (r,r), halo of r)
+    // one CG iteration: sweep A (+ all-reduce of (p,Ap); on slabs A also
+    // forms p on the halo planes), sweep B (+ all-reduce of (r,r), halo of r)
     auto iterate = [&](int it) -> cfd_status_t {
         double* pnew = P[it & 1];
         double* pold = P[(it + 1) & 1];
@@ -339,13 +341,19 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         if (D) {
             ST_TRY(reduce_dot(c));
             hipLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1, it);
-            ST_TRY(halo(c, {pnew}));
         }
         timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); });
         if (D) {
+            // r's halo goes out on the side stream (halo communicator) while
+            // the main stream all-reduces (r,r); the next sweep A waits for both
+            HIP_TRY(hipEventRecord(c->ev_b, c->stream));
+            HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
+            double* rr[1] = {c->r};
+            ST_TRY(c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false));
+            HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
             ST_TRY(reduce_dot(c));
             hipLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1, it);
-            ST_TRY(halo(c, {c->r}));
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
         }
         return CFD_SUCCESS;
     };
@@ -578,6 +586,12 @@ static void free_ctx(hip_proj_ctx* c) {
     for (int i = 0; i < 2; i++)
         if (c->ev_poll[i]) hipEventDestroy(c->ev_poll[i]);
     for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->ev_b) hipEventDestroy(c->ev_b);
+    if (c->ev_h) hipEventDestroy(c->ev_h);
+    if (c->hstream) {
+        hipStreamSynchronize(c->hstream);
+        hipStreamDestroy(c->hstream);
+    }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -669,6 +683,11 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     HIP_TRY(hipHostMalloc((void**)&c->h_red, 8 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_poll[0], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_poll[1], hipEventDisableTiming));
+    if (c->nranks > 1) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_b, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_h, hipEventDisableTiming));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return CFD_SUCCESS;
 }

@@ -44,8 +44,11 @@ namespace {
 // 8-B ncclAllReduce. Everything is stream-ordered on the caller's stream.
 // ---------------------------------------------------------------------------
 struct RcclComm final : SlabComm {
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;   // all-reduces
+    ncclComm_t hcomm = nullptr;  // halo send/recv: its own communicator, so a
+                                 // halo on a side stream may overlap an all-reduce
     ~RcclComm() override {
+        if (hcomm) ncclCommDestroy(hcomm);
         if (comm) ncclCommDestroy(comm);
     }
     // Posting order matters only when both neighbours are the same peer
@@ -58,10 +61,10 @@ struct RcclComm final : SlabComm {
         const int lo = lower(periodic), hi = upper(periodic);
         NCCLC(ncclGroupStart());
         for (int q = 0; q < nf; ++q) {
-            if (lo >= 0) NCCLC(ncclSend(f[q] + ps, (size_t)ps, ncclDouble, lo, comm, s));
-            if (hi >= 0) NCCLC(ncclSend(f[q] + ps * (nz - 2), (size_t)ps, ncclDouble, hi, comm, s));
-            if (hi >= 0) NCCLC(ncclRecv(f[q] + ps * (nz - 1), (size_t)ps, ncclDouble, hi, comm, s));
-            if (lo >= 0) NCCLC(ncclRecv(f[q], (size_t)ps, ncclDouble, lo, comm, s));
+            if (lo >= 0) NCCLC(ncclSend(f[q] + ps, (size_t)ps, ncclDouble, lo, hcomm, s));
+            if (hi >= 0) NCCLC(ncclSend(f[q] + ps * (nz - 2), (size_t)ps, ncclDouble, hi, hcomm, s));
+            if (hi >= 0) NCCLC(ncclRecv(f[q] + ps * (nz - 1), (size_t)ps, ncclDouble, hi, hcomm, s));
+            if (lo >= 0) NCCLC(ncclRecv(f[q], (size_t)ps, ncclDouble, lo, hcomm, s));
         }
         NCCLC(ncclGroupEnd());
         return CFD_SUCCESS;
@@ -251,6 +254,13 @@ hip_proj_comm_t* hip_proj_comm_create_rccl(const unsigned char id[HIP_PROJ_UNIQU
     if (r != ncclSuccess) {
         fail(CFD_ERROR, "ncclCommInitRank", ncclGetErrorString(r));
         c->comm = nullptr;
+        delete c;
+        return nullptr;
+    }
+    r = ncclCommSplit(c->comm, 0, rank, &c->hcomm, nullptr);
+    if (r != ncclSuccess) {
+        fail(CFD_ERROR, "ncclCommSplit", ncclGetErrorString(r));
+        c->hcomm = nullptr;
         delete c;
         return nullptr;
     }

@@ -1,0 +1,60 @@
+"""The committed fixtures in tests/golden/ against the oracle (CPU) and the
+reference vectors they descend from."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from cfd_amd import _abi as A
+from cfd_amd import api
+from oracle import oracle
+from tests import cases
+
+GOLD = Path(__file__).resolve().parent / "golden"
+F4 = ("u", "v", "w", "p")
+
+
+def load(name):
+    return np.load(GOLD / name, allow_pickle=False)
+
+
+def test_reference_vectors_match_cases():
+    ref = json.loads((GOLD / "reference_vectors.json").read_text())["projection_kat16_l2"]
+    assert (ref["u"], ref["v"], ref["p"]) == cases.KAT_PROJECTION_L2
+
+
+def test_kat_fixture_reproduces_reference_l2():
+    z = load("kat16_projection_step1.npz")
+    l2 = (cases.l2_rms(z["u"]), cases.l2_rms(z["v"]), cases.l2_rms(z["p"]))
+    assert l2 == cases.KAT_PROJECTION_L2
+
+
+@pytest.mark.parametrize("name,kind,tol", [
+    ("cavity17_rbsor_tol1e-2_3steps.npz", A.ORACLE_POISSON_REDBLACK, 1e-2),
+    ("cavity17_cg_3steps.npz", A.ORACLE_POISSON_CG, None)])
+def test_cavity_fixtures_regenerate_bitwise(name, kind, tol):
+    z = load(name)
+    g, f, p = cases.cavity(17, 17, 17, Re=100.0, dt=5e-4)
+    oracle.set_threads(1)
+    if tol:
+        oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=tol))
+    try:
+        for i in range(3):
+            api.cavity_bc(f, 1.0)
+            s, _, it = oracle.projection_step(f, g, p, kind)
+            assert s == A.CFD_SUCCESS and it == z["iters"][i]
+    finally:
+        oracle.set_projection_poisson_params(None)
+    for k in F4:
+        np.testing.assert_array_equal(getattr(f, k), z[k], err_msg=k)
+
+
+def test_poisson_fixture_regenerates_bitwise():
+    z = load("poisson17_cos.npz")
+    g, rhs = cases.cos_rhs(17)
+    np.testing.assert_array_equal(rhs, z["rhs"])
+    x = np.zeros_like(rhs)
+    s, st = oracle.redblack_solve(x, rhs, g.dx, g.dy, g.dz)
+    assert st.iterations == z["iters_rbsor"]
+    np.testing.assert_array_equal(x, z["x_rbsor"])

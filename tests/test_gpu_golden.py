@@ -1,0 +1,100 @@
+"""The HIP path against the committed golden fixtures (tests/golden/),
+independently of the live oracle: bitwise where the algorithm has no
+summation (RB-SOR, Jacobi), 1e-10 relative where CG dot products are summed
+in a different order."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from cfd_amd import _abi as A
+from cfd_amd import api
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+GOLD = Path(__file__).resolve().parent / "golden"
+F4 = {"u": A.HIP_FIELD_U, "v": A.HIP_FIELD_V, "w": A.HIP_FIELD_W, "p": A.HIP_FIELD_P}
+
+
+def load(name):
+    return np.load(GOLD / name, allow_pickle=False)
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b))))
+
+
+def _cavity_device(ctx, g, f, p, n):
+    for k, fid in F4.items():
+        ctx.set_field(fid, getattr(f, k))
+    ctx.set_density(1.0)
+    its = []
+    for _ in range(n):
+        ctx.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
+        ctx.apply_dirichlet(A.HIP_FIELD_V, api.dirichlet())
+        ctx.apply_dirichlet(A.HIP_FIELD_W, api.dirichlet())
+        ctx.apply_scalar_bc(A.HIP_FIELD_P, A.BC_TYPE_NEUMANN)
+        assert ctx.step_device(g, p) == A.CFD_SUCCESS, api._native.last_error()
+        its.append(ctx.poisson_stats().iterations)
+    return its, {k: ctx.get_field(fid) for k, fid in F4.items()}
+
+
+def test_cavity_rbsor_fixture_bitwise(hip_lib):
+    z = load("cavity17_rbsor_tol1e-2_3steps.npz")
+    g, f, p = cases.cavity(17, 17, 17, Re=100.0, dt=5e-4)
+    ctx = api.HipProjection(17, 17, 17, poisson_method=A.HIP_POISSON_REDBLACK,
+                            poisson_tolerance=1e-2)
+    its, out = _cavity_device(ctx, g, f, p, 3)
+    ctx.close()
+    assert its == list(z["iters"])
+    for k in F4:
+        np.testing.assert_array_equal(out[k], z[k], err_msg=k)
+
+
+def test_cavity_cg_fixture(hip_lib):
+    z = load("cavity17_cg_3steps.npz")
+    g, f, p = cases.cavity(17, 17, 17, Re=100.0, dt=5e-4)
+    ctx = api.HipProjection(17, 17, 17)
+    its, out = _cavity_device(ctx, g, f, p, 3)
+    ctx.close()
+    assert all(abs(a - b) <= 1 for a, b in zip(its, z["iters"]))
+    for k in F4:
+        assert _rel(out[k], z[k]) <= 1e-10, k
+
+
+def test_kat_fixture_via_plugin(hip_lib):
+    z = load("kat16_projection_step1.npz")
+    g, f, p = cases.kat_2d()
+    reg = api.Registry()
+    s = reg.create("projection_hip")
+    assert s.init(g, p) == A.CFD_SUCCESS
+    assert s.step(f, g, p, A.SolverStats()) == A.CFD_SUCCESS
+    s.close()
+    for k in ("u", "v", "w", "p"):
+        assert _rel(getattr(f, k), z[k]) <= 1e-12, k
+
+
+@pytest.mark.parametrize("method,key", [(A.HIP_POISSON_REDBLACK, "rbsor"),
+                                        (A.HIP_POISSON_JACOBI, "jacobi"),
+                                        (A.HIP_POISSON_CG, "cg")])
+def test_poisson_fixture(hip_lib, method, key):
+    z = load("poisson17_cos.npz")
+    rhs = z["rhs"]
+    d = 1.0 / 16
+    ctx = api.HipProjection(17, 17, 17)
+    x = np.zeros_like(rhs)
+    prm = None
+    if key == "jacobi":
+        prm = A.PoissonParams(1e-6, 1e-10, 3000, 0.0, 1, False, 0)
+    s, st = ctx.poisson_solve(method, x, rhs, d, d, d, prm)
+    ctx.close()
+    assert s == int(z[f"status_{key}"])
+    if key == "cg":
+        assert abs(st.iterations - int(z["iters_cg"])) <= 1
+        ref = z["x_cg"]
+        dd = (x - x.mean()) - (ref - ref.mean())
+        assert float(np.max(np.abs(dd))) / float(np.max(np.abs(ref))) < 1e-9
+    else:
+        assert st.iterations == int(z[f"iters_{key}"])
+        np.testing.assert_array_equal(x, z[f"x_{key}"])
