@@ -116,6 +116,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_apply_scalar_bc", C.c_int, V, C.c_int, C.c_int)
     _sig(lib, "hip_proj_apply_dirichlet", C.c_int, V, C.c_int, P(A.DirichletValues))
     _sig(lib, "hip_proj_get_poisson_stats", C.c_int, V, P(A.PoissonStats))
+    _sig(lib, "hip_proj_apply_thermal_bcs", C.c_int, V, P(A.SolverParams))
     _sig(lib, "hip_proj_enable_timing", None, V, C.c_int)
     _sig(lib, "hip_proj_reset_timing", None, V)
     _sig(lib, "hip_proj_get_timing", None, V, A.c_double_p, P(C.c_longlong))

@@ -834,13 +834,14 @@ __global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
     }
 }
 
-// Max over a full field (stats: max temperature, solver_registry.c:52-62).
+// Max over a full field (stats: max temperature, solver_registry.c:52-62),
+// planes [k_first, k_first + gridDim.z).
 __global__ __launch_bounds__(256) void k_field_max(Geo g, const double* __restrict__ f,
-                                                   unsigned long long* out) {
+                                                   unsigned long long* out, int k_first) {
     __shared__ double sh[4];
     const int i = blockIdx.x * 64 + (threadIdx.x & 63);
     const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int k = blockIdx.z;
+    const int k = k_first + (int)blockIdx.z;
     double m = -INFINITY;
     if (i < g.nx && j < g.ny) {
         double v = f[cidx(g, i, j, k)];
@@ -852,6 +853,111 @@ __global__ __launch_bounds__(256) void k_field_max(Geo g, const double* __restri
     if (threadIdx.x == 0) {
         double a = fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
         atomicMax(out, ord_enc(a));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Energy equation (energy_solver.c:21-176): explicit Euler on the corrected
+// velocity, T_new = T + dt(-(u.grad)T + alpha lap T), boundary cells copied;
+// any non-finite T_new sets red[5] (the reference's CFD_ERROR_DIVERGED scan).
+// 40 B/cell: read T (stencil), u, v, w; write T_new.
+// ---------------------------------------------------------------------------
+struct EnergyCoef {
+    double inv_2dx, inv_2dy, inv_2dz, inv_dx2, inv_dy2, inv_dz2, alpha, dt;
+};
+
+__global__ __launch_bounds__(256) void k_energy(Geo g, EnergyCoef ec, const double* __restrict__ T,
+                                                const double* __restrict__ U,
+                                                const double* __restrict__ V,
+                                                const double* __restrict__ W,
+                                                double* __restrict__ Tn,
+                                                unsigned long long* red) {
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    if (i >= g.nx || j >= g.ny) return;
+    const long long idx = cidx(g, i, j, k);
+    const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
+                           k >= g.k0 && k < g.k1);
+    double tn;
+    if (interior) {
+        const long long px = g.px, sz = g.sz;
+        const double Tc = T[idx];
+        double dT_dx = (T[idx + 1] - T[idx - 1]) * ec.inv_2dx;
+        double dT_dy = (T[idx + px] - T[idx - px]) * ec.inv_2dy;
+        double dT_dz = (T[idx + sz] - T[idx - sz]) * ec.inv_2dz;
+        double adv = U[idx] * dT_dx + V[idx] * dT_dy + W[idx] * dT_dz;
+        double d2x = (T[idx + 1] - 2.0 * Tc + T[idx - 1]) * ec.inv_dx2;
+        double d2y = (T[idx + px] - 2.0 * Tc + T[idx - px]) * ec.inv_dy2;
+        double d2z = (T[idx + sz] - 2.0 * Tc + T[idx - sz]) * ec.inv_dz2;
+        double diff = ec.alpha * (d2x + d2y + d2z);
+        double dT = ec.dt * (-adv + diff + 0.0);
+        tn = Tc + dT;
+    } else {
+        tn = T[idx];
+    }
+    Tn[idx] = tn;
+    if (!isfinite(tn)) atomicOr(&red[5], 1ull);
+}
+
+// Thermal boundary conditions (energy_solver.c:204-334), in the reference's
+// face order as three gather passes: pass 0 = left/right (x faces, every
+// local plane), pass 1 = bottom/top (reads the x-face values pass 0 wrote),
+// pass 2 = back/front (whole planes, edge ranks only). Types per face:
+// 0 periodic, 1 Neumann, 2 Dirichlet (bc_type_t); -1 = leave the face.
+struct ThermalFaces {
+    int type[6];   // left, right, bottom, top, back, front
+    double val[6];
+};
+
+__global__ __launch_bounds__(256) void k_thermal_bc(Geo g, double* __restrict__ T, ThermalFaces tf,
+                                                    int pass) {
+    const long long plane = (long long)g.nx * g.ny;
+    long long total;
+    if (pass == 0) total = 2LL * g.ny * g.nz;
+    else if (pass == 1) total = 2LL * g.nx * g.nz;
+    else total = 2LL * plane;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        int i, j, k, face;
+        if (pass == 0) {
+            face = (int)(e % 2);           // 0 left, 1 right
+            long long q = e / 2;
+            j = (int)(q % g.ny);
+            k = (int)(q / g.ny);
+            i = face == 0 ? 0 : g.nx - 1;
+        } else if (pass == 1) {
+            face = 2 + (int)(e % 2);       // 2 bottom, 3 top
+            long long q = e / 2;
+            i = (int)(q % g.nx);
+            k = (int)(q / g.nx);
+            j = face == 2 ? 0 : g.ny - 1;
+        } else {
+            face = 4 + (int)(e / plane);   // 4 back, 5 front
+            if ((face == 4 && !g.lo_face) || (face == 5 && !g.hi_face)) continue;
+            long long q = e % plane;
+            j = (int)(q / g.nx);
+            i = (int)(q % g.nx);
+            k = face == 4 ? 0 : g.nz - 1;
+        }
+        const int t = tf.type[face];
+        if (t < 0) continue;
+        const long long dst = cidx(g, i, j, k);
+        if (t == 2) {
+            T[dst] = tf.val[face];
+            continue;
+        }
+        int si = i, sj = j, sk = k;
+        const bool per = (t == 0);
+        switch (face) {
+            case 0: si = per ? g.nx - 2 : 1; break;
+            case 1: si = per ? 1 : g.nx - 2; break;
+            case 2: sj = per ? g.ny - 2 : 1; break;
+            case 3: sj = per ? 1 : g.ny - 2; break;
+            case 4: sk = per ? g.nz - 2 : 1; break;
+            default: sk = per ? 1 : g.nz - 2; break;
+        }
+        T[dst] = T[cidx(g, si, sj, sk)];
     }
 }
 

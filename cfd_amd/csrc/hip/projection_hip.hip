@@ -14,6 +14,7 @@
 
 #include "cfd_hip/projection_hip.h"
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,6 +53,7 @@ namespace {
 struct TimedLaunch {
     hipEvent_t a, b;
     int kind;
+    int iter;  // CG iteration of a sweep launch, -1 otherwise
 };
 
 }  // namespace
@@ -80,6 +82,7 @@ struct hip_proj_ctx {
     double *us = nullptr, *vs = nullptr, *ws = nullptr, *pn = nullptr;
     double *r = nullptr, *pa = nullptr, *pb = nullptr;
     double *rhs = nullptr, *xt = nullptr;
+    double* Tn = nullptr;  // energy equation output (swapped with T)
     double *src_u_row = nullptr, *src_v_col = nullptr;
     std::vector<double> h_src_u, h_src_v;
     // reductions / state
@@ -93,13 +96,17 @@ struct hip_proj_ctx {
     double rho0 = 1.0;
     double max_T = 0.0;
     int have_T = 0;
+    int T_dirty = 0;  // T changed since max_T was computed
     poisson_solver_stats_t pstats{};
     size_t bytes = 0;
+    std::vector<void*> allocs;  // hipMalloc bases of the field arrays
+    size_t stagger_bytes = 0;
     // timing
     int timing = 0;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<TimedLaunch> pending;
+    hipEvent_t ta = nullptr, tb = nullptr;  // events of the launch being timed
     double kt_ms[HIP_KT_COUNT] = {0};
     long long kt_n[HIP_KT_COUNT] = {0};
 };
@@ -107,10 +114,17 @@ struct hip_proj_ctx {
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
+// Field arrays start at staggered offsets (k-th allocation shifted by
+// k * stagger bytes, a multiple of 256 B) so that the streams a sweep reads
+// and writes at the same index do not all begin on the same HBM channel.
 static cfd_status_t dalloc(hip_proj_ctx* c, double** ptr, size_t n) {
-    HIP_TRY(hipMalloc((void**)ptr, n * sizeof(double)));
+    const size_t off = (size_t)c->allocs.size() * c->stagger_bytes;
+    void* base = nullptr;
+    HIP_TRY(hipMalloc(&base, n * sizeof(double) + off));
+    c->allocs.push_back(base);
+    *ptr = (double*)((char*)base + off);
     HIP_TRY(hipMemsetAsync(*ptr, 0, n * sizeof(double), c->stream));
-    c->bytes += n * sizeof(double);
+    c->bytes += n * sizeof(double) + off;
     return CFD_SUCCESS;
 }
 
@@ -136,8 +150,11 @@ static hipEvent_t take_event(hip_proj_ctx* c) {
     return c->ev_pool[c->ev_used++];
 }
 
-static void flush_timing(hip_proj_ctx* c) {
+// cg_limit: CG sweep launches of iterations >= cg_limit ran after convergence
+// (launched ahead of the host poll, they return at once) and are not counted.
+static void flush_timing(hip_proj_ctx* c, int cg_limit = 0x7fffffff) {
     for (auto& t : c->pending) {
+        if (t.iter >= cg_limit) continue;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
             c->kt_ms[t.kind] += ms;
@@ -148,10 +165,13 @@ static void flush_timing(hip_proj_ctx* c) {
     c->ev_used = 0;
 }
 
-// Record events around a launch when timing is enabled. The pool is flushed
+// Time a launch when timing is enabled: the kernel launched inside `launch`
+// goes through hipExtLaunchKernelGGL with the context's (ta, tb), so the
+// start/stop timestamps are taken by the dispatch packet itself (the kernel's
+// own duration, no extra marker packets in the stream). The pool is flushed
 // at every host synchronisation point.
 template <typename F>
-static void timed(hip_proj_ctx* c, int kind, F&& launch) {
+static void timed(hip_proj_ctx* c, int kind, F&& launch, int iter = -1) {
     if (!c->timing) {
         launch();
         return;
@@ -161,10 +181,11 @@ static void timed(hip_proj_ctx* c, int kind, F&& launch) {
         launch();
         return;
     }
-    hipEventRecord(a, c->stream);
+    c->ta = a;
+    c->tb = b;
     launch();
-    hipEventRecord(b, c->stream);
-    c->pending.push_back({a, b, kind});
+    c->ta = c->tb = nullptr;
+    c->pending.push_back({a, b, kind, iter});
 }
 
 static int tile_grid(const hip_proj_ctx* c) {
@@ -181,13 +202,13 @@ static bool dist(const hip_proj_ctx* c) { return c->nranks > 1; }
 template <int TY, bool FIRST, bool DIST>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
                          double* pn, double* x, int it) {
-    hipLaunchKernelGGL((k_cgA<TY, FIRST, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream,
+    hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream, c->ta, c->tb, 0,
                        c->sgeo, L, r, po, pn, x, c->st, c->partials, c->counter, it, c->dsum);
 }
 
 template <int TY, bool DIST>
 static void launch_cgB_t(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    hipLaunchKernelGGL((k_cgB<TY, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream,
+    hipExtLaunchKernelGGL((k_cgB<TY, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream, c->ta, c->tb, 0,
                        c->sgeo, L, p, r, c->st, c->partials, c->counter, it, c->dsum);
 }
 
@@ -225,7 +246,7 @@ static unsigned shell_blocks(const hip_proj_ctx* c) {
 }
 
 static void launch_bc(hip_proj_ctx* c, double* f, int mode, const DirVals& dv) {
-    hipLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->geo, f,
+    hipExtLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, f,
                        mode, dv);
 }
 
@@ -234,6 +255,7 @@ static __global__ void k_init_red(unsigned long long* red) {
         red[0] = 0x8000000000000000ull;  // enc(+0.0): reference maxima start at 0.0
         red[1] = 0x8000000000000000ull;
         red[2] = 0ull;
+        red[5] = 0ull;
         red[3] = 0x000FFFFFFFFFFFFFull;  // enc(-inf)
         red[4] = 0x8000000000000000ull;
     }
@@ -283,6 +305,9 @@ static const unsigned long long* reduce_red(hip_proj_ctx* c, cfd_status_t* st) {
         if (s_ != CFD_SUCCESS) return s_;       \
     } while (0)
 
+static cfd_status_t apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t& t,
+                                      bool is3d);
+
 // ---------------------------------------------------------------------------
 // pressure solvers on ctx->pn
 // ---------------------------------------------------------------------------
@@ -303,31 +328,31 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         const double* rhs_in = (src == RHS_FROM_VELOCITY) ? nullptr : c->rhs;
         if (src == RHS_FROM_VELOCITY) {
             if (D)
-                hipLaunchKernelGGL((k_cg_setup<true, false, true, true>), dim3(G), dim3(NT), 0,
-                                   c->stream, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
+                hipExtLaunchKernelGGL((k_cg_setup<true, false, true, true>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->ta, c->tb, 0, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
                                    c->r, c->st, c->partials, c->counter, rel_tol, abs_tol,
                                    max_iter, check_interval, c->dsum);
             else
-                hipLaunchKernelGGL((k_cg_setup<true, false, true, false>), dim3(G), dim3(NT), 0,
-                                   c->stream, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
+                hipExtLaunchKernelGGL((k_cg_setup<true, false, true, false>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->ta, c->tb, 0, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
                                    c->r, c->st, c->partials, c->counter, rel_tol, abs_tol,
                                    max_iter, check_interval, c->dsum);
         } else {
             if (D)
-                hipLaunchKernelGGL((k_cg_setup<false, false, true, true>), dim3(G), dim3(NT), 0,
-                                   c->stream, c->geo, L, dc, nullptr, nullptr, nullptr,
+                hipExtLaunchKernelGGL((k_cg_setup<false, false, true, true>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->ta, c->tb, 0, c->geo, L, dc, nullptr, nullptr, nullptr,
                                    (double*)rhs_in, x, c->r, c->st, c->partials, c->counter,
                                    rel_tol, abs_tol, max_iter, check_interval, c->dsum);
             else
-                hipLaunchKernelGGL((k_cg_setup<false, false, true, false>), dim3(G), dim3(NT), 0,
-                                   c->stream, c->geo, L, dc, nullptr, nullptr, nullptr,
+                hipExtLaunchKernelGGL((k_cg_setup<false, false, true, false>), dim3(G), dim3(NT), 0,
+                                   c->stream, c->ta, c->tb, 0, c->geo, L, dc, nullptr, nullptr, nullptr,
                                    (double*)rhs_in, x, c->r, c->st, c->partials, c->counter,
                                    rel_tol, abs_tol, max_iter, check_interval, c->dsum);
         }
     });
     if (D) {
         ST_TRY(reduce_dot(c));
-        hipLaunchKernelGGL(k_finish_setup, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1,
+        hipExtLaunchKernelGGL(k_finish_setup, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1,
                            rel_tol, abs_tol, max_iter, check_interval);
         ST_TRY(halo(c, {c->r}));
     }
@@ -337,12 +362,13 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     auto iterate = [&](int it) -> cfd_status_t {
         double* pnew = P[it & 1];
         double* pold = P[(it + 1) & 1];
-        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, x, it); });
+        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, x, it); },
+              it);
         if (D) {
             ST_TRY(reduce_dot(c));
-            hipLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1, it);
+            hipExtLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
         }
-        timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); });
+        timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); }, it);
         if (D) {
             // r's halo goes out on the side stream (halo communicator) while
             // the main stream all-reduces (r,r); the next sweep A waits for both
@@ -352,7 +378,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
             ST_TRY(c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false));
             HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
             ST_TRY(reduce_dot(c));
-            hipLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 1, it);
+            hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
         }
         return CFD_SUCCESS;
@@ -382,13 +408,13 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         slot ^= 1;
         chunk = std::min(chunk * 2, chunk_max);
     }
-    hipLaunchKernelGGL(k_cg_finalize, dim3(G), dim3(NT), 0, c->stream, c->geo, P[0], P[1], x,
+    hipExtLaunchKernelGGL(k_cg_finalize, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, P[0], P[1], x,
                        c->st);
     HIP_TRY(hipMemcpyAsync(&c->h_state[2], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    flush_timing(c);
     const CgState& s = c->h_state[2];
+    flush_timing(c, s.iterations);
     const bool stagnated = (s.status == ST_STAGNATED);
     // final poisson_solver_apply_bc (cg.c:447); the breakdown exit skips it.
     if (final_bc && !stagnated && !(s.iterations == 0 && s.status == ST_CONVERGED))
@@ -417,9 +443,9 @@ static double optimal_omega(size_t nx, size_t ny, size_t nz, double dx, double d
 
 static cfd_status_t residual_linf(hip_proj_ctx* c, const double* x, const ResCoef& rc, double* out) {
     const int G = tile_grid(c);
-    hipLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->red);
+    hipExtLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->red);
     timed(c, HIP_KT_RESIDUAL, [&] {
-        hipLaunchKernelGGL(k_residual_linf, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, x, c->rhs,
+        hipExtLaunchKernelGGL(k_residual_linf, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, rc, x, c->rhs,
                            c->red + 4);
     });
     cfd_status_t st;
@@ -465,17 +491,17 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     for (iter = 0; iter < max_iter; ++iter) {
         if (method == HIP_POISSON_REDBLACK) {
             timed(c, HIP_KT_RELAX, [&] {
-                hipLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
+                hipExtLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, rc, c->pn,
                                    c->rhs, 1);
             });
             ST_TRY(halo(c, {c->pn}));  // the black pass reads the neighbours' red cells
             timed(c, HIP_KT_RELAX, [&] {
-                hipLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
+                hipExtLaunchKernelGGL(k_rb_pass, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, rc, c->pn,
                                    c->rhs, 0);
             });
         } else {
             timed(c, HIP_KT_RELAX, [&] {
-                hipLaunchKernelGGL(k_jacobi, dim3(G), dim3(NT), 0, c->stream, c->geo, rc, c->pn,
+                hipExtLaunchKernelGGL(k_jacobi, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, rc, c->pn,
                                    c->xt, c->rhs);
             });
             // memcpy(x, x_temp) + BC == swap buffers then BC (all boundary
@@ -534,8 +560,27 @@ static cfd_status_t validate_params(const hip_proj_ctx* c, const grid* g,
         return CFD_ERROR_UNSUPPORTED;
     }
     if (prm->alpha > 0.0) {
-        set_err(CFD_ERROR_UNSUPPORTED, "projection_hip: energy equation not enabled in this build");
-        return CFD_ERROR_UNSUPPORTED;
+        if (prm->heat_source_func) {  // host callback (gpu_shared_kernels.cuh:271-276)
+            set_err(CFD_ERROR_UNSUPPORTED,
+                    "projection_hip: host heat_source_func callbacks cannot run on the device");
+            return CFD_ERROR_UNSUPPORTED;
+        }
+        const ns_thermal_bc_config_t& t = prm->thermal_bc;
+        auto ok = [](bc_type_t b) {
+            return b == BC_TYPE_PERIODIC || b == BC_TYPE_NEUMANN || b == BC_TYPE_DIRICHLET;
+        };
+        if (!ok(t.left) || !ok(t.right) || !ok(t.bottom) || !ok(t.top) ||
+            (g->nz > 1 && (!ok(t.front) || !ok(t.back)))) {  // energy_solver.c:230-241
+            set_err(CFD_ERROR_INVALID,
+                    "energy_apply_thermal_bcs: unsupported thermal BC type on a face "
+                    "(only PERIODIC, NEUMANN, DIRICHLET are valid)");
+            return CFD_ERROR_INVALID;
+        }
+        if (c->nranks > 1 && ((t.back == BC_TYPE_PERIODIC) != (t.front == BC_TYPE_PERIODIC))) {
+            set_err(CFD_ERROR_UNSUPPORTED,
+                    "projection_hip: Z-slabs need periodic thermal BCs on both z faces or neither");
+            return CFD_ERROR_UNSUPPORTED;
+        }
     }
     return CFD_SUCCESS;
 }
@@ -571,10 +616,7 @@ int hip_projection_available(void) {
 static void free_ctx(hip_proj_ctx* c) {
     if (!c) return;
     if (c->stream) hipStreamSynchronize(c->stream);
-    double* bufs[] = {c->u,  c->v,  c->w,   c->p,  c->T,   c->us,       c->vs,       c->ws,
-                      c->pn, c->r,  c->pa,  c->pb, c->rhs, c->xt, c->src_u_row, c->src_v_col};
-    for (double* b : bufs)
-        if (b) hipFree(b);
+    for (void* b : c->allocs) hipFree(b);
     if (c->st) hipFree(c->st);
     if (c->partials) hipFree(c->partials);
     if (c->counter) hipFree(c->counter);
@@ -602,6 +644,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, c->device));
     c->grid_cap = std::max(64, prop.multiProcessorCount * 8);
+    if (const char* e = getenv("CFD_HIP_FIELD_STAGGER")) c->stagger_bytes = (size_t)atol(e) / 256 * 256;
     c->nx = nx;
     c->ny = ny;
     c->nz = nz;
@@ -796,7 +839,7 @@ cfd_status_t hip_proj_set_field(hip_proj_ctx_t* c, int id, const double* host) {
                              c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
                              c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (id == HIP_FIELD_T) c->have_T = 1;
+    if (id == HIP_FIELD_T) c->have_T = c->T_dirty = 1;
     return CFD_SUCCESS;
 }
 
@@ -828,9 +871,10 @@ cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
     }
     if (!d) return CFD_ERROR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
-    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, c->stream, d,
+    hipExtLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, c->stream, c->ta, c->tb, 0, d,
                        (long long)field_elems(c), value);
     HIP_TRY(hipGetLastError());
+    if (id == HIP_FIELD_T) c->T_dirty = 1;
     return CFD_SUCCESS;
 }
 
@@ -850,11 +894,6 @@ cfd_status_t hip_proj_upload(hip_proj_ctx_t* c, const flow_field* f) {
     if ((s = hip_proj_set_field(c, HIP_FIELD_P, f->p)) != CFD_SUCCESS) return s;
     if (f->T) {
         if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
-        size_t n = c->nx * c->ny * c->nz;
-        double m = f->T[0];
-        for (size_t i = 1; i < n; i++)
-            if (f->T[i] > m) m = f->T[i];
-        c->max_T = m;
     }
     c->rho0 = f->rho ? f->rho[0] : 1.0;
     return CFD_SUCCESS;
@@ -887,7 +926,7 @@ cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type)
         // z copy (plane 0 <- nz-2, nz-1 <- 1) as a wrap-around halo exchange
         Geo g = c->geo;
         g.lo_face = g.hi_face = 0;
-        hipLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, g, d, mode,
+        hipExtLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta, c->tb, 0, g, d, mode,
                            DirVals{});
         HIP_TRY(hipGetLastError());
         return halo(c, {d}, true);
@@ -905,6 +944,19 @@ cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* c, int id, const bc_dirich
     HIP_TRY(hipSetDevice(c->device));
     launch_bc(c, d, 2, dv);
     HIP_TRY(hipGetLastError());
+    return CFD_SUCCESS;
+}
+
+cfd_status_t hip_proj_apply_thermal_bcs(hip_proj_ctx_t* c, const ns_solver_params_t* prm) {
+    if (!c || !prm) return CFD_ERROR_INVALID;
+    if (!c->T) {
+        set_err(CFD_ERROR_INVALID, "energy_apply_thermal_bcs: missing temperature field");
+        return CFD_ERROR_INVALID;
+    }
+    if (prm->alpha <= 0.0) return CFD_SUCCESS;  // energy disabled: no-op (energy_solver.c:217)
+    HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(apply_thermal_bcs(c, prm->thermal_bc, c->nzg > 1));
+    c->T_dirty = 1;
     return CFD_SUCCESS;
 }
 
@@ -938,6 +990,38 @@ void hip_proj_get_timing(hip_proj_ctx_t* c, double* total_ms, long long* launche
     }
 }
 
+// energy_apply_thermal_bcs (energy_solver.c:204-334) on the device T:
+// x faces, y faces, z faces (3-D), each a gather pass in the reference order.
+static cfd_status_t apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t& t, bool is3d) {
+    ThermalFaces tf;
+    const bc_type_t ty[6] = {t.left, t.right, t.bottom, t.top, t.back, t.front};
+    const double v[6] = {t.dirichlet_values.left, t.dirichlet_values.right,
+                         t.dirichlet_values.bottom, t.dirichlet_values.top,
+                         t.dirichlet_values.back, t.dirichlet_values.front};
+    for (int f = 0; f < 6; ++f) {
+        tf.type[f] = (ty[f] == BC_TYPE_PERIODIC || ty[f] == BC_TYPE_NEUMANN ||
+                      ty[f] == BC_TYPE_DIRICHLET) ? (int)ty[f] : -1;
+        tf.val[f] = v[f];
+    }
+    auto blocks = [](long long n) {
+        return (unsigned)std::max(1LL, std::min((n + 255) / 256, 65535LL));
+    };
+    hipExtLaunchKernelGGL(k_thermal_bc, dim3(blocks(2LL * c->ny * c->nz)), dim3(256), 0, c->stream, c->ta, c->tb, 0,
+                       c->geo, c->T, tf, 0);
+    hipExtLaunchKernelGGL(k_thermal_bc, dim3(blocks(2LL * c->nx * c->nz)), dim3(256), 0, c->stream, c->ta, c->tb, 0,
+                       c->geo, c->T, tf, 1);
+    if (is3d) {
+        if (dist(c) && t.back == BC_TYPE_PERIODIC && t.front == BC_TYPE_PERIODIC) {
+            ST_TRY(halo(c, {c->T}, true));  // z wrap across the slabs
+        } else {
+            hipExtLaunchKernelGGL(k_thermal_bc, dim3(blocks(2LL * c->nx * c->ny)), dim3(256), 0,
+                               c->stream, c->ta, c->tb, 0, c->geo, c->T, tf, 2);
+        }
+    }
+    HIP_TRY(hipGetLastError());
+    return CFD_SUCCESS;
+}
+
 static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                      const ns_solver_params_t* prm, ns_solver_stats_t* stats,
                                      int iter) {
@@ -950,9 +1034,14 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     const double dz = (nz > 1 && g->dz) ? g->dz[0] : 0.0;
     const double dt = prm->dt;
     const bool buoy = (prm->beta != 0.0);
-    if (buoy && !c->have_T) {
-        set_err(CFD_ERROR_INVALID, "projection_hip: Boussinesq buoyancy needs the T field");
+    const bool energy = (prm->alpha > 0.0);
+    if ((buoy || energy) && !c->have_T) {
+        set_err(CFD_ERROR_INVALID, "projection_hip: buoyancy / energy equation need the T field");
         return CFD_ERROR_INVALID;
+    }
+    if (energy && !c->Tn) {
+        s = dalloc(c, &c->Tn, field_elems(c));
+        if (s != CFD_SUCCESS) return s;
     }
 
     // source-term tables: compute_source_terms at iter = 0 (solver_explicit_euler.c:317-333)
@@ -986,13 +1075,13 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     const dim3 cg = cell_grid(c);
     // slabs: the neighbours' planes of everything the stencils read
     ST_TRY(halo(c, {c->u, c->v, c->w, c->p}));
-    if (buoy) ST_TRY(halo(c, {c->T}));
+    if (buoy || energy) ST_TRY(halo(c, {c->T}));
     timed(c, HIP_KT_PREDICTOR, [&] {
         if (buoy)
-            hipLaunchKernelGGL(k_predictor<true>, cg, dim3(256), 0, c->stream, c->geo, pc, c->u,
+            hipExtLaunchKernelGGL(k_predictor<true>, cg, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, pc, c->u,
                                c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
         else
-            hipLaunchKernelGGL(k_predictor<false>, cg, dim3(256), 0, c->stream, c->geo, pc, c->u,
+            hipExtLaunchKernelGGL(k_predictor<false>, cg, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, pc, c->u,
                                c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
     });
     HIP_TRY(hipGetLastError());
@@ -1021,7 +1110,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
         if (s != CFD_SUCCESS) return s;
         const Lap L = make_lap(dx, dy, dz);
         const int G = tile_grid(c);
-        hipLaunchKernelGGL((k_cg_setup<true, true, false>), dim3(G), dim3(NT), 0, c->stream,
+        hipExtLaunchKernelGGL((k_cg_setup<true, true, false>), dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0,
                            c->geo, L, dc, c->us, c->vs, c->ws, c->rhs, c->pn, c->r, c->st,
                            c->partials, c->counter, 0.0, 0.0, 0, 1, c->dsum);
         if (method == HIP_POISSON_JACOBI)
@@ -1041,24 +1130,58 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     cc.two_dy = 2.0 * dy;
     cc.inv_2dz = pc.inv_2dz;
     cc.dt_over_rho = dt / rho;
-    hipLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->red);
+    hipExtLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->red);
     timed(c, HIP_KT_CORRECTOR, [&] {
         const int ks = (c->nz > 1 && !c->geo.lo_face) ? 1 : 0;
         const int ke = (c->nz > 1 && !c->geo.hi_face) ? (int)c->nz - 1 : (int)c->nz;
         const dim3 cgz(cg.x, cg.y, (unsigned)((ke - ks + CORR_KC - 1) / CORR_KC));
-        hipLaunchKernelGGL(k_corrector, cgz, dim3(256), 0, c->stream, c->geo, cc, c->us, c->vs,
+        hipExtLaunchKernelGGL(k_corrector, cgz, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, cc, c->us, c->vs,
                            c->ws, c->pn, c->u, c->v, c->w, c->red);
     });
     std::swap(c->p, c->pn);  // memcpy(field->p, p_new) (solver_projection.c:253)
+    if (energy) {
+        // energy_step_explicit on the corrected velocity (solver_projection.c:255-265)
+        EnergyCoef ec;
+        ec.inv_2dx = 1.0 / (2.0 * dx);
+        ec.inv_2dy = 1.0 / (2.0 * dy);
+        ec.inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * dz) : 0.0;
+        ec.inv_dx2 = 1.0 / (dx * dx);
+        ec.inv_dy2 = 1.0 / (dy * dy);
+        ec.inv_dz2 = (nz > 1 && g->dz) ? 1.0 / (dz * dz) : 0.0;
+        ec.alpha = prm->alpha;
+        ec.dt = dt;
+        timed(c, HIP_KT_ENERGY, [&] {
+            hipExtLaunchKernelGGL(k_energy, cg, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, ec, c->T, c->u,
+                               c->v, c->w, c->Tn, c->red);
+        });
+        std::swap(c->T, c->Tn);
+        ST_TRY(apply_thermal_bcs(c, prm->thermal_bc, nz > 1));  // :267-274
+        c->T_dirty = 1;
+    }
+    if (c->have_T && c->T_dirty) {
+        // compute_max_temperature (solver_registry.c:52-62), owned planes + faces
+        const int ks = (c->nz > 1 && !c->geo.lo_face) ? 1 : 0;
+        const int ke = (c->nz > 1 && !c->geo.hi_face) ? (int)c->nz - 1 : (int)c->nz;
+        hipExtLaunchKernelGGL(k_field_max, dim3(cg.x, cg.y, (unsigned)(ke - ks)), dim3(256), 0,
+                           c->stream, c->ta, c->tb, 0, c->geo, c->T, c->red + 3, ks);
+    }
     const unsigned long long* red = reduce_red(c, &s);
     if (s != CFD_SUCCESS) return s;
     HIP_TRY(hipMemcpyAsync(c->h_red, red, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     flush_timing(c);
+    if (c->h_red[5]) {
+        set_err(CFD_ERROR_DIVERGED, "NaN/Inf detected in energy_step_explicit");
+        return CFD_ERROR_DIVERGED;
+    }
     if (c->h_red[2]) {
         set_err(CFD_ERROR_DIVERGED, "projection_hip: NaN/Inf in the flow field");
         return CFD_ERROR_DIVERGED;
+    }
+    if (c->have_T && c->T_dirty) {
+        c->max_T = ord_dec(c->h_red[3]);
+        c->T_dirty = 0;
     }
     if (stats) {
         stats->iterations = 1;
@@ -1102,6 +1225,10 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter
     if (s == CFD_SUCCESS || s == CFD_ERROR_DIVERGED) {
         cfd_status_t d = hip_proj_download(c, f);
         if (d != CFD_SUCCESS) return d;
+        if (prm->alpha > 0.0 && f->T && c->T) {
+            d = hip_proj_get_field(c, HIP_FIELD_T, f->T);
+            if (d != CFD_SUCCESS) return d;
+        }
     }
     if (s == CFD_SUCCESS && stats && f->T) {
         // compute_max_temperature (solver_registry.c:52-62) on the host copy

@@ -80,7 +80,8 @@ typedef enum {
     HIP_KT_CORRECTOR = 4,
     HIP_KT_RELAX = 5,      /* one RB-SOR colour pass or one Jacobi sweep */
     HIP_KT_RESIDUAL = 6,   /* L-infinity residual for the relaxation methods */
-    HIP_KT_COUNT = 7
+    HIP_KT_ENERGY = 7,     /* energy equation (alpha > 0) */
+    HIP_KT_COUNT = 8
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);
@@ -123,6 +124,11 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* ctx, int fi
                                                      bc_type_t type);
 CFD_HIP_EXPORT cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* ctx, int field_id,
                                                      const bc_dirichlet_values_t* values);
+
+/* energy_apply_thermal_bcs (energy_solver.c:204-334) on the device T with
+ * params->thermal_bc; a no-op when params->alpha <= 0, as in the reference. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_apply_thermal_bcs(hip_proj_ctx_t* ctx,
+                                                       const ns_solver_params_t* params);
 
 /* Pressure-solver statistics of the most recent step. */
 CFD_HIP_EXPORT cfd_status_t hip_proj_get_poisson_stats(hip_proj_ctx_t* ctx,

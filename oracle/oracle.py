@@ -69,6 +69,9 @@ def lib():
         sig("oracle_field_destroy", None, P(A.FlowField))
         sig("oracle_params_default", A.SolverParams)
         sig("oracle_max_velocity_pressure", None, P(A.FlowField), d, d)
+        sig("oracle_apply_thermal_bcs", C.c_int, P(A.FlowField), P(A.SolverParams))
+        sig("oracle_energy_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
+            C.c_double, C.c_double)
         _lib = L
     return _lib
 
@@ -137,6 +140,11 @@ def jacobi_solve(x, rhs, dx, dy, dz, params=None):
 def cg_fixed_iters(x, rhs, dx, dy, dz, iters) -> float:
     nz, ny, nx = x.shape
     return lib().oracle_cg_fixed_iters(_dp(x), _dp(rhs), nx, ny, nz, dx, dy, dz, iters)
+
+
+def apply_thermal_bcs(field, params) -> int:
+    """energy_apply_thermal_bcs (energy_solver.c:204-334) on field.T."""
+    return lib().oracle_apply_thermal_bcs(field.ptr, C.byref(params))
 
 
 def bc_neumann(a: np.ndarray):

@@ -82,8 +82,21 @@ def poisson():
     np.savez_compressed(HERE / "poisson17_cos.npz", rhs=rhs, **out)
 
 
+def dvd_ra1e3():
+    """de Vahl Davis Ra=1e3 on 41^2 (test_natural_convection.c:315-322)."""
+    import json
+
+    from tests import dvd
+    g, f, p, alpha = dvd.setup(41, 1000.0, 0.002)
+    r = dvd.run(lambda ff: oracle.projection_step(ff, g, p)[0], g, f, p, alpha, 30000)
+    r = {k: (float(v) if not isinstance(v, bool) else v) for k, v in r.items()}
+    (HERE / "dvd41_ra1e3.json").write_text(json.dumps(r, indent=1) + "\n")
+    np.savez_compressed(HERE / "dvd41_ra1e3_fields.npz", u=f.u, v=f.v, p=f.p, T=f.T)
+
+
 if __name__ == "__main__":
     oracle.set_threads(1)
+    dvd_ra1e3()
     kat()
     cavity_rbsor()
     cavity_cg()
