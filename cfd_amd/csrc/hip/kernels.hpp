@@ -383,6 +383,29 @@ __device__ __forceinline__ void st2(double* p, long long i, double2 v) {
     *reinterpret_cast<double2*>(p + i) = v;
 }
 
+// Sweep variants (template FL): bit 0 = non-temporal stores of the streamed
+// outputs, bit 1 = non-temporal loads of inputs no other tile reads.
+constexpr int SW_NT_STORE = 1;
+constexpr int SW_NT_LOAD = 2;
+typedef double d2x __attribute__((ext_vector_type(2)));
+template <int FL>
+__device__ __forceinline__ void st2v(double* p, long long i, double2 v) {
+    if (FL & SW_NT_STORE) {
+        d2x w = {v.x, v.y};
+        __builtin_nontemporal_store(w, reinterpret_cast<d2x*>(p + i));
+    } else {
+        *reinterpret_cast<double2*>(p + i) = v;
+    }
+}
+template <int FL>
+__device__ __forceinline__ double2 ld2v(const double* p, long long i) {
+    if (FL & SW_NT_LOAD) {
+        d2x w = __builtin_nontemporal_load(reinterpret_cast<const d2x*>(p + i));
+        return make_double2(w.x, w.y);
+    }
+    return *reinterpret_cast<const double2*>(p + i);
+}
+
 struct RowPair {
     int i0, j, kb, ke, lane, w;
     bool act, in0, in1;
@@ -415,7 +438,7 @@ __device__ __forceinline__ RowPair row_pair(const SGeo& g) {
 
 // Sweep A (iteration it):  p_it = r + beta p_{it-1} (FIRST: p = r), written
 // to pnew; (p, A p) with A p in registers; deferred x += alpha_{it-1} p_{it-1}.
-template <int TY, bool FIRST, bool DIST>
+template <int TY, bool FIRST, bool DIST, int FL = 0>
 __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __restrict__ r,
                                                  const double* __restrict__ po,
                                                  double* __restrict__ pn, double* __restrict__ x,
@@ -459,7 +482,7 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
         double2 op = (xok && !FIRST) ? ld2(po, ip) : zero;
         double2 rp = xok ? ld2(r, ip) : zero;
         double2 hp = (xok && halo && k + 1 < c.ke) ? PV(ip + hoff) : zero;
-        double2 xo = (xok && !FIRST) ? ld2(x, idx) : zero;
+        double2 xo = (xok && !FIRST) ? ld2v<FL>(x, idx) : zero;
         double el = (c.lane == 0 && c.i0 >= 1 && xok) ? PS(idx - 1) : 0.0;
         double er = (c.lane == 63 && c.i0 + 2 < g.nx) ? PS(idx + 2) : 0.0;
         rows[buf][c.w + 1][c.lane] = pc;
@@ -478,12 +501,12 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
             double2 pw;
             pw.x = c.in0 ? pc.x : 0.0;
             pw.y = c.in1 ? pc.y : 0.0;
-            st2(pn, idx, pw);
+            st2v<FL>(pn, idx, pw);
             if (!FIRST) {
                 double2 xw;
                 xw.x = c.in0 ? xo.x + alpha * oc.x : xo.x;
                 xw.y = c.in1 ? xo.y + alpha * oc.y : xo.y;
-                st2(x, idx, xw);
+                st2v<FL>(x, idx, xw);
             }
         }
         if (c.in0) acc += pc.x * Ap0;
@@ -519,7 +542,7 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
 
 // Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
 // to sweep A's), rho_new = (r, r), convergence test and beta.
-template <int TY, bool DIST>
+template <int TY, bool DIST, int FL = 0>
 __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
                                                  double* __restrict__ r, CgState* st,
                                                  double* partials, unsigned* counter, int it,
@@ -546,7 +569,7 @@ __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __
         const long long ip = idx + g.sz;
         double2 pp = xok ? ld2(p, ip) : zero;
         double2 hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
-        double2 rr = xok ? ld2(r, idx) : zero;
+        double2 rr = xok ? ld2v<FL>(r, idx) : zero;
         double el = (c.lane == 0 && c.i0 >= 1 && xok) ? p[idx - 1] : 0.0;
         double er = (c.lane == 63 && c.i0 + 2 < g.nx) ? p[idx + 2] : 0.0;
         rows[buf][c.w + 1][c.lane] = pc;
@@ -563,7 +586,7 @@ __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __
         double2 rn;
         rn.x = c.in0 ? rr.x + malpha * Ap0 : rr.x;
         rn.y = c.in1 ? rr.y + malpha * Ap1 : rr.y;
-        if (c.act) st2(r, idx, rn);
+        if (c.act) st2v<FL>(r, idx, rn);
         if (c.in0) acc += rn.x * rn.x;
         if (c.in1) acc += rn.y * rn.y;
         pm = pc;

@@ -66,6 +66,7 @@ struct hip_proj_ctx {
     Geo geo{};
     SGeo sgeo{};       // row-pair CG sweep tiling
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
+    int sweep_variant = 0;  // SW_NT_* flags of the CG sweeps
     int grid_cap = 2048;
     hip_proj_config_t cfg{};
     // Z-slab decomposition (nranks == 1: the whole grid, no communicator)
@@ -199,39 +200,56 @@ static int sweep_grid(const hip_proj_ctx* c) {
 
 static bool dist(const hip_proj_ctx* c) { return c->nranks > 1; }
 
-template <int TY, bool FIRST, bool DIST>
+template <int TY, bool FIRST, bool DIST, int FL>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
                          double* pn, double* x, int it) {
-    hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream, c->ta, c->tb, 0,
-                       c->sgeo, L, r, po, pn, x, c->st, c->partials, c->counter, it, c->dsum);
+    hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST, FL>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
+                          c->stream, c->ta, c->tb, 0, c->sgeo, L, r, po, pn, x, c->st,
+                          c->partials, c->counter, it, c->dsum);
 }
 
-template <int TY, bool DIST>
+template <int TY, bool DIST, int FL>
 static void launch_cgB_t(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    hipExtLaunchKernelGGL((k_cgB<TY, DIST>), dim3(sweep_grid(c)), dim3(64 * TY), 0, c->stream, c->ta, c->tb, 0,
-                       c->sgeo, L, p, r, c->st, c->partials, c->counter, it, c->dsum);
+    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
+                          c->stream, c->ta, c->tb, 0, c->sgeo, L, p, r, c->st, c->partials,
+                          c->counter, it, c->dsum);
 }
 
+template <int TY, int FL>
+static void launch_cgA_f(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
+                         const double* po, double* pn, double* x, int it) {
+    const bool d = dist(c);
+    if (first) d ? launch_cgA_t<TY, true, true, FL>(c, L, r, po, pn, x, it)
+                 : launch_cgA_t<TY, true, false, FL>(c, L, r, po, pn, x, it);
+    else d ? launch_cgA_t<TY, false, true, FL>(c, L, r, po, pn, x, it)
+           : launch_cgA_t<TY, false, false, FL>(c, L, r, po, pn, x, it);
+}
+
+template <int TY, int FL>
+static void launch_cgB_f(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
+    dist(c) ? launch_cgB_t<TY, true, FL>(c, L, p, r, it) : launch_cgB_t<TY, false, FL>(c, L, p, r, it);
+}
+
+// sweep_ty 4 or 8; sweep_variant selects the SW_NT_* flags (TY 8 only)
 static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
                        const double* po, double* pn, double* x, int it) {
-    const bool d = dist(c);
-    if (c->sweep_ty == 4) {
-        if (first) d ? launch_cgA_t<4, true, true>(c, L, r, po, pn, x, it)
-                     : launch_cgA_t<4, true, false>(c, L, r, po, pn, x, it);
-        else d ? launch_cgA_t<4, false, true>(c, L, r, po, pn, x, it)
-               : launch_cgA_t<4, false, false>(c, L, r, po, pn, x, it);
-    } else {
-        if (first) d ? launch_cgA_t<8, true, true>(c, L, r, po, pn, x, it)
-                     : launch_cgA_t<8, true, false>(c, L, r, po, pn, x, it);
-        else d ? launch_cgA_t<8, false, true>(c, L, r, po, pn, x, it)
-               : launch_cgA_t<8, false, false>(c, L, r, po, pn, x, it);
+    if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, x, it);
+    switch (c->sweep_variant) {
+        case 1: return launch_cgA_f<8, 1>(c, first, L, r, po, pn, x, it);
+        case 2: return launch_cgA_f<8, 2>(c, first, L, r, po, pn, x, it);
+        case 3: return launch_cgA_f<8, 3>(c, first, L, r, po, pn, x, it);
+        default: return launch_cgA_f<8, 0>(c, first, L, r, po, pn, x, it);
     }
 }
 
 static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    const bool d = dist(c);
-    if (c->sweep_ty == 4) d ? launch_cgB_t<4, true>(c, L, p, r, it) : launch_cgB_t<4, false>(c, L, p, r, it);
-    else d ? launch_cgB_t<8, true>(c, L, p, r, it) : launch_cgB_t<8, false>(c, L, p, r, it);
+    if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, L, p, r, it);
+    switch (c->sweep_variant) {
+        case 1: return launch_cgB_f<8, 1>(c, L, p, r, it);
+        case 2: return launch_cgB_f<8, 2>(c, L, p, r, it);
+        case 3: return launch_cgB_f<8, 3>(c, L, p, r, it);
+        default: return launch_cgB_f<8, 0>(c, L, p, r, it);
+    }
 }
 
 static dim3 cell_grid(const hip_proj_ctx* c) {
@@ -678,6 +696,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
 
     // row-pair CG sweeps: 128 x TY x kc tiles (kernels.hpp, k_cgA / k_cgB)
     c->sweep_ty = (c->cfg.sweep_rows == 4) ? 4 : 8;
+    c->sweep_variant = c->cfg.sweep_variant & 3;
     SGeo& sg = c->sgeo;
     sg.nx = g.nx;
     sg.ny = g.ny;

@@ -58,6 +58,8 @@ typedef struct {
     int kchunk;                   /* z planes per CG sweep tile; 0 = auto (64) */
     int verbose;
     int sweep_rows;               /* y rows (wavefronts) per CG sweep workgroup: 4 or 8 */
+    int sweep_variant;            /* CG sweep memory hints: bit0 non-temporal stores,
+                                     bit1 non-temporal loads of single-use inputs */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;

@@ -87,12 +87,26 @@ def test_energy_steps_cg_vs_oracle(hip_lib, shape):
         assert float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b)))) <= 1e-10, k
 
 
+def _at_rest(f):
+    # RB-SOR runs the singular Neumann problem (linear_solver_redblack.c:139);
+    # a random velocity field's divergence is far from compatible with it, so
+    # these cases start at rest (buoyancy drives the flow) with the looser
+    # tolerance the cavity RB tests use.
+    f.u[...] = 0.0
+    f.v[...] = 0.0
+    f.w[...] = 0.0
+
+
+RB_TOL = 1e-2
+
+
 def test_energy_steps_rbsor_bitwise(hip_lib):
     g, f, p = _convection_case(17, 13, 11)
+    _at_rest(f)
     _thermal(p, (D, D, N, N, P, P))
-    oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=1e-3))
+    oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=RB_TOL))
     try:
-        fo = _steps(g, f, p, 4, method=A.HIP_POISSON_REDBLACK, poisson_tolerance=1e-3)
+        fo = _steps(g, f, p, 4, method=A.HIP_POISSON_REDBLACK, poisson_tolerance=RB_TOL)
     finally:
         oracle.set_projection_poisson_params(None)
     for k in ("u", "v", "w", "p", "T"):
@@ -106,10 +120,11 @@ def test_slab_energy_rbsor_bitwise(hip_lib, monkeypatch, nranks, zbc):
     the slabs)."""
     monkeypatch.setenv("CFD_HIP_GROUP_TIMEOUT_S", "60")
     g, f, p = _convection_case(17, 13, 11)
+    _at_rest(f)
     _thermal(p, (D, D, N, N, zbc, zbc))
     grp = api.LocalGroup(nranks)
     ctxs = [api.HipProjection(17, 13, 11, comm=grp.comm(r, 0),
-                              poisson_method=A.HIP_POISSON_REDBLACK, poisson_tolerance=1e-3)
+                              poisson_method=A.HIP_POISSON_REDBLACK, poisson_tolerance=RB_TOL)
             for r in range(nranks)]
     fid = {"u": A.HIP_FIELD_U, "v": A.HIP_FIELD_V, "w": A.HIP_FIELD_W, "p": A.HIP_FIELD_P,
            "T": A.HIP_FIELD_T}
@@ -137,7 +152,7 @@ def test_slab_energy_rbsor_bitwise(hip_lib, monkeypatch, nranks, zbc):
         for c in ctxs:
             c.close()
         grp.close()
-    oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=1e-3))
+    oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=RB_TOL))
     try:
         for _ in range(3):
             assert oracle.projection_step(f, g, p, A.ORACLE_POISSON_REDBLACK)[0] == A.CFD_SUCCESS
