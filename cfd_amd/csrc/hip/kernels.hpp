@@ -270,14 +270,14 @@ __device__ __forceinline__ void fin_B(CgState* st, double tot, int it) {
     }
 }
 
-__global__ void k_finish_setup(CgState* st, const double* tot, double rel_tol, double abs_tol,
+static __global__ void k_finish_setup(CgState* st, const double* tot, double rel_tol, double abs_tol,
                                int max_iter, int check_interval) {
     if (threadIdx.x == 0) fin_setup(st, tot[0], rel_tol, abs_tol, max_iter, check_interval);
 }
-__global__ void k_finish_A(CgState* st, const double* tot, int it) {
+static __global__ void k_finish_A(CgState* st, const double* tot, int it) {
     if (threadIdx.x == 0 && !st->done) fin_A(st, tot[0], it);
 }
-__global__ void k_finish_B(CgState* st, const double* tot, int it) {
+static __global__ void k_finish_B(CgState* st, const double* tot, int it) {
     if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it);
 }
 
@@ -295,7 +295,7 @@ struct DivCoef {
 };
 
 template <bool FROM_VEL, bool WRITE_RHS, bool WITH_RR, bool DIST = false>
-__global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
+static __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc,
                                                  const double* __restrict__ us,
                                                  const double* __restrict__ vs,
                                                  const double* __restrict__ ws,
@@ -439,7 +439,7 @@ __device__ __forceinline__ RowPair row_pair(const SGeo& g) {
 // Sweep A (iteration it):  p_it = r + beta p_{it-1} (FIRST: p = r), written
 // to pnew; (p, A p) with A p in registers; deferred x += alpha_{it-1} p_{it-1}.
 template <int TY, bool FIRST, bool DIST, int FL = 0>
-__global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __restrict__ r,
+static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __restrict__ r,
                                                  const double* __restrict__ po,
                                                  double* __restrict__ pn, double* __restrict__ x,
                                                  CgState* st, double* partials, unsigned* counter,
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __
 // Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
 // to sweep A's), rho_new = (r, r), convergence test and beta.
 template <int TY, bool DIST, int FL = 0>
-__global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
+static __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
                                                  double* __restrict__ r, CgState* st,
                                                  double* partials, unsigned* counter, int it,
                                                  double* dsum) {
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __
 
 // Apply the deferred x += alpha p of the last iteration when the reference
 // would have applied it (converged, rho breakdown, max iterations).
-__global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, const double* __restrict__ p0,
+static __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, const double* __restrict__ p0,
                                                     const double* __restrict__ p1,
                                                     double* __restrict__ x, const CgState* st) {
     if (!st->pending || st->iterations <= 0) return;
@@ -647,7 +647,7 @@ __device__ __forceinline__ int bc_map(int c, int n, int mode) {
 // In a Z-slab the z faces exist only on the edge ranks (lo_face / hi_face);
 // the x/y ring is applied on every local plane, halo planes included (their
 // owner applies the identical gather to the same values).
-__global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f, int mode,
+static __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f, int mode,
                                                   DirVals dv) {
     const bool is3d = g.nz > 1;
     const bool lo = is3d && g.lo_face, hi = is3d && g.hi_face;
@@ -710,7 +710,7 @@ struct PredCoef {
 };
 
 template <bool BUOY>
-__global__ __launch_bounds__(256) void k_predictor(Geo g, PredCoef pc,
+static __global__ __launch_bounds__(256) void k_predictor(Geo g, PredCoef pc,
                                                    const double* __restrict__ U,
                                                    const double* __restrict__ V,
                                                    const double* __restrict__ W,
@@ -789,7 +789,7 @@ struct CorrCoef {
 };
 constexpr int CORR_KC = 64;  // planes per corrector workgroup
 
-__global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
+static __global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
                                                    const double* __restrict__ us,
                                                    const double* __restrict__ vs,
                                                    const double* __restrict__ ws,
@@ -859,7 +859,7 @@ __global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
 
 // Max over a full field (stats: max temperature, solver_registry.c:52-62),
 // planes [k_first, k_first + gridDim.z).
-__global__ __launch_bounds__(256) void k_field_max(Geo g, const double* __restrict__ f,
+static __global__ __launch_bounds__(256) void k_field_max(Geo g, const double* __restrict__ f,
                                                    unsigned long long* out, int k_first) {
     __shared__ double sh[4];
     const int i = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -889,7 +889,7 @@ struct EnergyCoef {
     double inv_2dx, inv_2dy, inv_2dz, inv_dx2, inv_dy2, inv_dz2, alpha, dt;
 };
 
-__global__ __launch_bounds__(256) void k_energy(Geo g, EnergyCoef ec, const double* __restrict__ T,
+static __global__ __launch_bounds__(256) void k_energy(Geo g, EnergyCoef ec, const double* __restrict__ T,
                                                 const double* __restrict__ U,
                                                 const double* __restrict__ V,
                                                 const double* __restrict__ W,
@@ -933,7 +933,7 @@ struct ThermalFaces {
     double val[6];
 };
 
-__global__ __launch_bounds__(256) void k_thermal_bc(Geo g, double* __restrict__ T, ThermalFaces tf,
+static __global__ __launch_bounds__(256) void k_thermal_bc(Geo g, double* __restrict__ T, ThermalFaces tf,
                                                     int pass) {
     const long long plane = (long long)g.nx * g.ny;
     long long total;
@@ -996,7 +996,7 @@ struct RelaxCoef {
     double dx2, dy2, inv_dz2, inv_factor, omega;
 };
 
-__global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __restrict__ x,
+static __global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __restrict__ x,
                                                 const double* __restrict__ rhs, int parity) {
     const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -1015,7 +1015,7 @@ __global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __r
     }
 }
 
-__global__ __launch_bounds__(NT) void k_jacobi(Geo g, RelaxCoef rc, const double* __restrict__ xin,
+static __global__ __launch_bounds__(NT) void k_jacobi(Geo g, RelaxCoef rc, const double* __restrict__ xin,
                                                double* __restrict__ xout,
                                                const double* __restrict__ rhs) {
     const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
@@ -1037,7 +1037,7 @@ struct ResCoef {
     double dx2, dy2, inv_dz2;
 };
 
-__global__ __launch_bounds__(NT) void k_residual_linf(Geo g, ResCoef rc,
+static __global__ __launch_bounds__(NT) void k_residual_linf(Geo g, ResCoef rc,
                                                       const double* __restrict__ x,
                                                       const double* __restrict__ rhs,
                                                       unsigned long long* out) {

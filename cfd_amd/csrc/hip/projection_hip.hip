@@ -9,196 +9,7 @@
 // host only polls a pinned copy of the state every few iterations, so there
 // is no host round trip per iteration (the reference GPU path does two per
 // iteration, poisson_cg_gpu_solve.cuh:189-203).
-#include "kernels.hpp"
-#include "slab_comm.hpp"
-
-#include "cfd_hip/projection_hip.h"
-
-#include <hip/hip_ext.h>
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cmath>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <initializer_list>
-#include <vector>
-
-using namespace cfdhip;
-
-// Error reporting goes through the host library's thread-local error state
-// (cfd_set_error, logging.c:39-46 in the reference). Weak, so the library
-// links against either the reference's host library or ours.
-extern "C" void cfd_set_error(cfd_status_t status, const char* message) __attribute__((weak));
-
-static void set_err(cfd_status_t s, const char* msg) {
-    if (cfd_set_error) cfd_set_error(s, msg);
-}
-
-#define HIP_TRY(call)                                                              \
-    do {                                                                           \
-        hipError_t e_ = (call);                                                    \
-        if (e_ != hipSuccess) {                                                    \
-            char buf_[256];                                                        \
-            snprintf(buf_, sizeof(buf_), "HIP error %s at %s:%d (%s)",             \
-                     hipGetErrorString(e_), __FILE__, __LINE__, #call);            \
-            set_err(CFD_ERROR, buf_);                                              \
-            return CFD_ERROR;                                                      \
-        }                                                                          \
-    } while (0)
-
-namespace {
-
-struct TimedLaunch {
-    hipEvent_t a, b;
-    int kind;
-    int iter;  // CG iteration of a sweep launch, -1 otherwise
-};
-
-}  // namespace
-
-struct hip_proj_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    size_t nx = 0, ny = 0, nz = 0;
-    long long px = 0, ps = 0;
-    Geo geo{};
-    SGeo sgeo{};       // row-pair CG sweep tiling
-    int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
-    int sweep_variant = 0;  // SW_NT_* flags of the CG sweeps
-    int grid_cap = 2048;
-    hip_proj_config_t cfg{};
-    // Z-slab decomposition (nranks == 1: the whole grid, no communicator)
-    SlabComm* comm = nullptr;
-    int rank = 0, nranks = 1;
-    size_t nzg = 0;    // global nz
-    size_t kofs = 0;   // global index of local plane 0
-    double* dsum = nullptr;            // [0] local dot total, [1] all-reduced
-    hipStream_t hstream = nullptr;     // side stream: halo of r overlaps the (r,r) all-reduce
-    hipEvent_t ev_b = nullptr, ev_h = nullptr;
-    unsigned long long* redg = nullptr;  // all-reduced red[]
-    // fields
-    double *u = nullptr, *v = nullptr, *w = nullptr, *p = nullptr, *T = nullptr;
-    double *us = nullptr, *vs = nullptr, *ws = nullptr, *pn = nullptr;
-    double *r = nullptr, *pa = nullptr, *pb = nullptr;
-    double *rhs = nullptr, *xt = nullptr;
-    double* Tn = nullptr;  // energy equation output (swapped with T)
-    double *src_u_row = nullptr, *src_v_col = nullptr;
-    std::vector<double> h_src_u, h_src_v;
-    // reductions / state
-    CgState* st = nullptr;
-    double* partials = nullptr;
-    unsigned* counter = nullptr;
-    unsigned long long* red = nullptr;   // [0] max vel, [1] max |p|, [2] nonfinite, [3] max T, [4] residual
-    CgState* h_state = nullptr;          // pinned, 2 slots + final
-    unsigned long long* h_red = nullptr; // pinned, 8
-    hipEvent_t ev_poll[2] = {nullptr, nullptr};
-    double rho0 = 1.0;
-    double max_T = 0.0;
-    int have_T = 0;
-    int T_dirty = 0;  // T changed since max_T was computed
-    poisson_solver_stats_t pstats{};
-    size_t bytes = 0;
-    std::vector<void*> allocs;  // hipMalloc bases of the field arrays
-    size_t stagger_bytes = 0;
-    // timing
-    int timing = 0;
-    std::vector<hipEvent_t> ev_pool;
-    size_t ev_used = 0;
-    std::vector<TimedLaunch> pending;
-    hipEvent_t ta = nullptr, tb = nullptr;  // events of the launch being timed
-    double kt_ms[HIP_KT_COUNT] = {0};
-    long long kt_n[HIP_KT_COUNT] = {0};
-};
-
-// ---------------------------------------------------------------------------
-// small helpers
-// ---------------------------------------------------------------------------
-// Field arrays start at staggered offsets (k-th allocation shifted by
-// k * stagger bytes, a multiple of 256 B) so that the streams a sweep reads
-// and writes at the same index do not all begin on the same HBM channel.
-static cfd_status_t dalloc(hip_proj_ctx* c, double** ptr, size_t n) {
-    const size_t off = (size_t)c->allocs.size() * c->stagger_bytes;
-    void* base = nullptr;
-    HIP_TRY(hipMalloc(&base, n * sizeof(double) + off));
-    c->allocs.push_back(base);
-    *ptr = (double*)((char*)base + off);
-    HIP_TRY(hipMemsetAsync(*ptr, 0, n * sizeof(double), c->stream));
-    c->bytes += n * sizeof(double) + off;
-    return CFD_SUCCESS;
-}
-
-static size_t field_elems(const hip_proj_ctx* c) { return (size_t)c->ps * c->nz; }
-
-static double* field_ptr(hip_proj_ctx* c, int id) {
-    switch (id) {
-        case HIP_FIELD_U: return c->u;
-        case HIP_FIELD_V: return c->v;
-        case HIP_FIELD_W: return c->w;
-        case HIP_FIELD_P: return c->p;
-        case HIP_FIELD_T: return c->T;
-        default: return nullptr;
-    }
-}
-
-static hipEvent_t take_event(hip_proj_ctx* c) {
-    if (c->ev_used == c->ev_pool.size()) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
-        c->ev_pool.push_back(e);
-    }
-    return c->ev_pool[c->ev_used++];
-}
-
-// cg_limit: CG sweep launches of iterations >= cg_limit ran after convergence
-// (launched ahead of the host poll, they return at once) and are not counted.
-static void flush_timing(hip_proj_ctx* c, int cg_limit = 0x7fffffff) {
-    for (auto& t : c->pending) {
-        if (t.iter >= cg_limit) continue;
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
-            c->kt_ms[t.kind] += ms;
-            c->kt_n[t.kind] += 1;
-        }
-    }
-    c->pending.clear();
-    c->ev_used = 0;
-}
-
-// Time a launch when timing is enabled: the kernel launched inside `launch`
-// goes through hipExtLaunchKernelGGL with the context's (ta, tb), so the
-// start/stop timestamps are taken by the dispatch packet itself (the kernel's
-// own duration, no extra marker packets in the stream). The pool is flushed
-// at every host synchronisation point.
-template <typename F>
-static void timed(hip_proj_ctx* c, int kind, F&& launch, int iter = -1) {
-    if (!c->timing) {
-        launch();
-        return;
-    }
-    hipEvent_t a = take_event(c), b = take_event(c);
-    if (!a || !b) {
-        launch();
-        return;
-    }
-    c->ta = a;
-    c->tb = b;
-    launch();
-    c->ta = c->tb = nullptr;
-    c->pending.push_back({a, b, kind, iter});
-}
-
-static int tile_grid(const hip_proj_ctx* c) {
-    long long nt = (long long)c->geo.tiles_x * c->geo.tiles_y * c->geo.tiles_z;
-    return (int)std::max(1LL, std::min<long long>(nt, c->grid_cap));
-}
-
-static int sweep_grid(const hip_proj_ctx* c) {
-    return c->sgeo.tiles_x * c->sgeo.tiles_y * c->sgeo.tiles_z;
-}
-
-static bool dist(const hip_proj_ctx* c) { return c->nranks > 1; }
+#include "ctx.hpp"
 
 template <int TY, bool FIRST, bool DIST, int FL>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
@@ -251,80 +62,6 @@ static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r
         default: return launch_cgB_f<8, 0>(c, L, p, r, it);
     }
 }
-
-static dim3 cell_grid(const hip_proj_ctx* c) {
-    return dim3((unsigned)((c->nx + 63) / 64), (unsigned)((c->ny + 3) / 4), (unsigned)c->nz);
-}
-
-static unsigned shell_blocks(const hip_proj_ctx* c) {
-    long long ring = 2LL * c->nx + 2LL * (c->ny - 2);
-    long long total = ring * (long long)c->nz + (c->nz > 1 ? 2LL * c->nx * c->ny : 0);
-    long long b = (total + 255) / 256;
-    return (unsigned)std::max(1LL, std::min(b, 65535LL));
-}
-
-static void launch_bc(hip_proj_ctx* c, double* f, int mode, const DirVals& dv) {
-    hipExtLaunchKernelGGL(k_bc_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, f,
-                       mode, dv);
-}
-
-static __global__ void k_init_red(unsigned long long* red) {
-    if (threadIdx.x == 0) {
-        red[0] = 0x8000000000000000ull;  // enc(+0.0): reference maxima start at 0.0
-        red[1] = 0x8000000000000000ull;
-        red[2] = 0ull;
-        red[5] = 0ull;
-        red[3] = 0x000FFFFFFFFFFFFFull;  // enc(-inf)
-        red[4] = 0x8000000000000000ull;
-    }
-}
-
-static double ord_dec(unsigned long long e) {
-    unsigned long long b = (e & 0x8000000000000000ull) ? (e & 0x7FFFFFFFFFFFFFFFull) : ~e;
-    double d;
-    memcpy(&d, &b, sizeof(d));
-    return d;
-}
-
-static Lap make_lap(double dx, double dy, double dz) {
-    Lap L;
-    L.dx2_inv = 1.0 / (dx * dx);
-    L.dy2_inv = 1.0 / (dy * dy);
-    L.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
-    return L;
-}
-
-// Refresh the halo planes of the given slab fields (no-op on one rank).
-static cfd_status_t halo(hip_proj_ctx* c, std::initializer_list<double*> fs,
-                         bool periodic = false) {
-    if (!dist(c)) return CFD_SUCCESS;
-    double* f[8];
-    int n = 0;
-    for (double* x : fs) f[n++] = x;
-    return c->comm->halo(c->stream, f, n, c->ps, (int)c->nz, periodic);
-}
-
-// Sum the per-rank dot total dsum[0] into dsum[1].
-static cfd_status_t reduce_dot(hip_proj_ctx* c) {
-    return c->comm->allreduce_sum(c->stream, c->dsum, c->dsum + 1, 1);
-}
-
-// Device copy of the maxima/flags in red[] that every rank agrees on.
-static const unsigned long long* reduce_red(hip_proj_ctx* c, cfd_status_t* st) {
-    *st = CFD_SUCCESS;
-    if (!dist(c)) return c->red;
-    *st = c->comm->allreduce_max_u64(c->stream, c->red, c->redg, 8);
-    return c->redg;
-}
-
-#define ST_TRY(expr)                            \
-    do {                                        \
-        cfd_status_t s_ = (expr);               \
-        if (s_ != CFD_SUCCESS) return s_;       \
-    } while (0)
-
-static cfd_status_t apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t& t,
-                                      bool is3d);
 
 // ---------------------------------------------------------------------------
 // pressure solvers on ctx->pn
@@ -558,7 +295,7 @@ static cfd_status_t ensure_aux(hip_proj_ctx* c, bool need_rhs, bool need_xt) {
     return CFD_SUCCESS;
 }
 
-static cfd_status_t validate_params(const hip_proj_ctx* c, const grid* g,
+cfd_status_t ctx_validate_params(const hip_proj_ctx* c, const grid* g,
                                     const ns_solver_params_t* prm) {
     if (!g || !prm) return CFD_ERROR_INVALID;
     if (g->nx != c->nx || g->ny != c->ny || g->nz != c->nzg) {
@@ -974,7 +711,7 @@ cfd_status_t hip_proj_apply_thermal_bcs(hip_proj_ctx_t* c, const ns_solver_param
     }
     if (prm->alpha <= 0.0) return CFD_SUCCESS;  // energy disabled: no-op (energy_solver.c:217)
     HIP_TRY(hipSetDevice(c->device));
-    ST_TRY(apply_thermal_bcs(c, prm->thermal_bc, c->nzg > 1));
+    ST_TRY(ctx_apply_thermal_bcs(c, prm->thermal_bc, c->nzg > 1));
     c->T_dirty = 1;
     return CFD_SUCCESS;
 }
@@ -1009,9 +746,11 @@ void hip_proj_get_timing(hip_proj_ctx_t* c, double* total_ms, long long* launche
     }
 }
 
+}  // extern "C"
+
 // energy_apply_thermal_bcs (energy_solver.c:204-334) on the device T:
 // x faces, y faces, z faces (3-D), each a gather pass in the reference order.
-static cfd_status_t apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t& t, bool is3d) {
+cfd_status_t ctx_apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t& t, bool is3d) {
     ThermalFaces tf;
     const bc_type_t ty[6] = {t.left, t.right, t.bottom, t.top, t.back, t.front};
     const double v[6] = {t.dirichlet_values.left, t.dirichlet_values.right,
@@ -1041,11 +780,49 @@ static cfd_status_t apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_confi
     return CFD_SUCCESS;
 }
 
+cfd_status_t ctx_energy_step(hip_proj_ctx* c, const grid* g, const ns_solver_params_t* prm) {
+    // energy_step_explicit_with_workspace (energy_solver.c:21-176) on the
+    // current velocity, then energy_apply_thermal_bcs (:204-334)
+    const size_t nz = c->nzg;
+    const double dx = g->dx[0], dy = g->dy[0];
+    const double dz = (nz > 1 && g->dz) ? g->dz[0] : 0.0;
+    if (!c->Tn) ST_TRY(dalloc(c, &c->Tn, field_elems(c)));
+    EnergyCoef ec;
+    ec.inv_2dx = 1.0 / (2.0 * dx);
+    ec.inv_2dy = 1.0 / (2.0 * dy);
+    ec.inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * dz) : 0.0;
+    ec.inv_dx2 = 1.0 / (dx * dx);
+    ec.inv_dy2 = 1.0 / (dy * dy);
+    ec.inv_dz2 = (nz > 1 && g->dz) ? 1.0 / (dz * dz) : 0.0;
+    ec.alpha = prm->alpha;
+    ec.dt = prm->dt;
+    timed(c, HIP_KT_ENERGY, [&] {
+        hipExtLaunchKernelGGL(k_energy, cell_grid(c), dim3(256), 0, c->stream, c->ta, c->tb, 0,
+                              c->geo, ec, c->T, c->u, c->v, c->w, c->Tn, c->red);
+    });
+    std::swap(c->T, c->Tn);
+    ST_TRY(ctx_apply_thermal_bcs(c, prm->thermal_bc, nz > 1));
+    c->T_dirty = 1;
+    return CFD_SUCCESS;
+}
+
+void ctx_queue_max_T(hip_proj_ctx* c) {
+    if (!c->have_T || !c->T_dirty) return;
+    // compute_max_temperature (solver_registry.c:52-62), owned planes + faces
+    const int ks = (c->nz > 1 && !c->geo.lo_face) ? 1 : 0;
+    const int ke = (c->nz > 1 && !c->geo.hi_face) ? (int)c->nz - 1 : (int)c->nz;
+    const dim3 cg = cell_grid(c);
+    hipLaunchKernelGGL(k_field_max, dim3(cg.x, cg.y, (unsigned)(ke - ks)), dim3(256), 0,
+                       c->stream, c->geo, c->T, c->red + 3, ks);
+}
+
+extern "C" {
+
 static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                      const ns_solver_params_t* prm, ns_solver_stats_t* stats,
                                      int iter) {
     if (!c) return CFD_ERROR_INVALID;
-    cfd_status_t s = validate_params(c, g, prm);
+    cfd_status_t s = ctx_validate_params(c, g, prm);
     if (s != CFD_SUCCESS) return s;
     HIP_TRY(hipSetDevice(c->device));
     const size_t nx = c->nx, ny = c->ny, nz = c->nzg;
@@ -1057,10 +834,6 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     if ((buoy || energy) && !c->have_T) {
         set_err(CFD_ERROR_INVALID, "projection_hip: buoyancy / energy equation need the T field");
         return CFD_ERROR_INVALID;
-    }
-    if (energy && !c->Tn) {
-        s = dalloc(c, &c->Tn, field_elems(c));
-        if (s != CFD_SUCCESS) return s;
     }
 
     // source-term tables: compute_source_terms at iter = 0 (solver_explicit_euler.c:317-333)
@@ -1158,32 +931,8 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                            c->ws, c->pn, c->u, c->v, c->w, c->red);
     });
     std::swap(c->p, c->pn);  // memcpy(field->p, p_new) (solver_projection.c:253)
-    if (energy) {
-        // energy_step_explicit on the corrected velocity (solver_projection.c:255-265)
-        EnergyCoef ec;
-        ec.inv_2dx = 1.0 / (2.0 * dx);
-        ec.inv_2dy = 1.0 / (2.0 * dy);
-        ec.inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * dz) : 0.0;
-        ec.inv_dx2 = 1.0 / (dx * dx);
-        ec.inv_dy2 = 1.0 / (dy * dy);
-        ec.inv_dz2 = (nz > 1 && g->dz) ? 1.0 / (dz * dz) : 0.0;
-        ec.alpha = prm->alpha;
-        ec.dt = dt;
-        timed(c, HIP_KT_ENERGY, [&] {
-            hipExtLaunchKernelGGL(k_energy, cg, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, ec, c->T, c->u,
-                               c->v, c->w, c->Tn, c->red);
-        });
-        std::swap(c->T, c->Tn);
-        ST_TRY(apply_thermal_bcs(c, prm->thermal_bc, nz > 1));  // :267-274
-        c->T_dirty = 1;
-    }
-    if (c->have_T && c->T_dirty) {
-        // compute_max_temperature (solver_registry.c:52-62), owned planes + faces
-        const int ks = (c->nz > 1 && !c->geo.lo_face) ? 1 : 0;
-        const int ke = (c->nz > 1 && !c->geo.hi_face) ? (int)c->nz - 1 : (int)c->nz;
-        hipExtLaunchKernelGGL(k_field_max, dim3(cg.x, cg.y, (unsigned)(ke - ks)), dim3(256), 0,
-                           c->stream, c->ta, c->tb, 0, c->geo, c->T, c->red + 3, ks);
-    }
+    if (energy) ST_TRY(ctx_energy_step(c, g, prm));  // solver_projection.c:255-274
+    ctx_queue_max_T(c);
     const unsigned long long* red = reduce_red(c, &s);
     if (s != CFD_SUCCESS) return s;
     HIP_TRY(hipMemcpyAsync(c->h_red, red, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
@@ -1225,7 +974,7 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter
     ns_solver_stats_t* stats, int n_steps) {
     if (!c || !f || !g || !prm) return CFD_ERROR_INVALID;
     if (f->nx < 3 || f->ny < 3 || (f->nz > 1 && f->nz < 3)) return CFD_ERROR_INVALID;
-    cfd_status_t s = validate_params(c, g, prm);
+    cfd_status_t s = ctx_validate_params(c, g, prm);
     if (s != CFD_SUCCESS) return s;
     if (n_steps <= 0) return CFD_SUCCESS;
     if ((s = hip_proj_set_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;

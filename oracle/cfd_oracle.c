@@ -988,3 +988,154 @@ done:
     free(us); free(vs); free(ws); free(pn); free(pt); free(rhs);
     return st;
 }
+
+/* ------------------------------------------------------------------------ */
+/* RK4 (solver_rk4.c:69-259) with the shared momentum RHS                    */
+/* (ns_momentum_rhs_scalar.h:49-190) and apply_boundary_conditions          */
+/* (solver_explicit_euler.c:231-306)                                         */
+/* ------------------------------------------------------------------------ */
+#define RK_MAX_D1 100.0    /* MAX_DERIVATIVE_LIMIT */
+#define RK_MAX_D2 1000.0   /* MAX_SECOND_DERIVATIVE_LIMIT */
+#define RK_MAX_DIV 10.0    /* MAX_DIVERGENCE_LIMIT */
+#define RK_P_FACTOR 0.1    /* PRESSURE_UPDATE_FACTOR */
+
+static inline double clampd(double x, double lim) { return fmax(-lim, fmin(lim, x)); }
+
+static void rk_rhs(const flow_field* f, const grid* g, const ns_solver_params_t* prm,
+                   double* ru, double* rv, double* rw, double* rp, int iter, double dt) {
+    size_t nx = f->nx, ny = f->ny, nz = f->nz, plane = nx * ny;
+    size_t sz = (nz > 1) ? plane : 0, k0 = (nz > 1) ? 1 : 0, k1 = (nz > 1) ? nz - 1 : 1;
+    double inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * g->dz[0]) : 0.0;
+    double inv_dz2 = (nz > 1 && g->dz) ? 1.0 / (g->dz[0] * g->dz[0]) : 0.0;
+    const double *u = f->u, *v = f->v, *w = f->w, *p = f->p, *rho = f->rho, *T = f->T;
+    PAR
+    for (size_t k = k0; k < k1; k++)
+        for (size_t j = 1; j < ny - 1; j++)
+            for (size_t i = 1; i < nx - 1; i++) {
+                size_t idx = k * sz + j * nx + i;
+                if (rho[idx] <= 1e-10 || fabs(g->dx[i]) < 1e-10 || fabs(g->dy[j]) < 1e-10) {
+                    ru[idx] = rv[idx] = rw[idx] = rp[idx] = 0.0;
+                    continue;
+                }
+                size_t il = (i > 1) ? idx - 1 : k * sz + j * nx + (nx - 2);
+                size_t ir = (i < nx - 2) ? idx + 1 : k * sz + j * nx + 1;
+                size_t jd = (j > 1) ? idx - nx : k * sz + (ny - 2) * nx + i;
+                size_t ju = (j < ny - 2) ? idx + nx : k * sz + 1 * nx + i;
+                size_t kd = (k > 1) ? idx - sz : (nz - 2) * sz + j * nx + i;
+                size_t ku = (k < nz - 2) ? idx + sz : 1 * sz + j * nx + i;
+                double tdx = 2.0 * g->dx[i], tdy = 2.0 * g->dy[j];
+                double dxx = g->dx[i] * g->dx[i], dyy = g->dy[j] * g->dy[j];
+                double du_dx = (u[ir] - u[il]) / tdx, du_dy = (u[ju] - u[jd]) / tdy;
+                double du_dz = (u[ku] - u[kd]) * inv_2dz;
+                double dv_dx = (v[ir] - v[il]) / tdx, dv_dy = (v[ju] - v[jd]) / tdy;
+                double dv_dz = (v[ku] - v[kd]) * inv_2dz;
+                double dw_dx = (w[ir] - w[il]) / tdx, dw_dy = (w[ju] - w[jd]) / tdy;
+                double dw_dz = (w[ku] - w[kd]) * inv_2dz;
+                double dp_dx = (p[ir] - p[il]) / tdx, dp_dy = (p[ju] - p[jd]) / tdy;
+                double dp_dz = (p[ku] - p[kd]) * inv_2dz;
+                double d2u_dx2 = (u[ir] - 2.0 * u[idx] + u[il]) / dxx;
+                double d2u_dy2 = (u[ju] - 2.0 * u[idx] + u[jd]) / dyy;
+                double d2u_dz2 = (u[ku] - 2.0 * u[idx] + u[kd]) * inv_dz2;
+                double d2v_dx2 = (v[ir] - 2.0 * v[idx] + v[il]) / dxx;
+                double d2v_dy2 = (v[ju] - 2.0 * v[idx] + v[jd]) / dyy;
+                double d2v_dz2 = (v[ku] - 2.0 * v[idx] + v[kd]) * inv_dz2;
+                double d2w_dx2 = (w[ir] - 2.0 * w[idx] + w[il]) / dxx;
+                double d2w_dy2 = (w[ju] - 2.0 * w[idx] + w[jd]) / dyy;
+                double d2w_dz2 = (w[ku] - 2.0 * w[idx] + w[kd]) * inv_dz2;
+                double nu = prm->mu / fmax(rho[idx], 1e-10);
+                nu = fmin(nu, 1.0);
+                du_dx = clampd(du_dx, RK_MAX_D1); du_dy = clampd(du_dy, RK_MAX_D1);
+                du_dz = clampd(du_dz, RK_MAX_D1); dv_dx = clampd(dv_dx, RK_MAX_D1);
+                dv_dy = clampd(dv_dy, RK_MAX_D1); dv_dz = clampd(dv_dz, RK_MAX_D1);
+                dw_dx = clampd(dw_dx, RK_MAX_D1); dw_dy = clampd(dw_dy, RK_MAX_D1);
+                dw_dz = clampd(dw_dz, RK_MAX_D1); dp_dx = clampd(dp_dx, RK_MAX_D1);
+                dp_dy = clampd(dp_dy, RK_MAX_D1); dp_dz = clampd(dp_dz, RK_MAX_D1);
+                d2u_dx2 = clampd(d2u_dx2, RK_MAX_D2); d2u_dy2 = clampd(d2u_dy2, RK_MAX_D2);
+                d2u_dz2 = clampd(d2u_dz2, RK_MAX_D2); d2v_dx2 = clampd(d2v_dx2, RK_MAX_D2);
+                d2v_dy2 = clampd(d2v_dy2, RK_MAX_D2); d2v_dz2 = clampd(d2v_dz2, RK_MAX_D2);
+                d2w_dx2 = clampd(d2w_dx2, RK_MAX_D2); d2w_dy2 = clampd(d2w_dy2, RK_MAX_D2);
+                d2w_dz2 = clampd(d2w_dz2, RK_MAX_D2);
+                /* compute_source_terms (solver_explicit_euler.c:317-333) + buoyancy */
+                double su = prm->source_amplitude_u * sin(M_PI * g->y[j]) *
+                            exp(-prm->source_decay_rate * iter * dt);
+                double sv = prm->source_amplitude_v * sin(2.0 * M_PI * g->x[i]) *
+                            exp(-prm->source_decay_rate * iter * dt);
+                double sw = 0.0;
+                if (T && prm->beta != 0.0) {
+                    double dT = T[idx] - prm->T_ref;
+                    su += -prm->beta * dT * prm->gravity[0];
+                    sv += -prm->beta * dT * prm->gravity[1];
+                    sw += -prm->beta * dT * prm->gravity[2];
+                }
+                ru[idx] = -u[idx] * du_dx - v[idx] * du_dy - w[idx] * du_dz - dp_dx / rho[idx] +
+                          nu * (d2u_dx2 + d2u_dy2 + d2u_dz2) + su;
+                rv[idx] = -u[idx] * dv_dx - v[idx] * dv_dy - w[idx] * dv_dz - dp_dy / rho[idx] +
+                          nu * (d2v_dx2 + d2v_dy2 + d2v_dz2) + sv;
+                rw[idx] = -u[idx] * dw_dx - v[idx] * dw_dy - w[idx] * dw_dz - dp_dz / rho[idx] +
+                          nu * (d2w_dx2 + d2w_dy2 + d2w_dz2) + sw;
+                double div = du_dx + dv_dy + dw_dz;
+                div = fmax(-RK_MAX_DIV, fmin(RK_MAX_DIV, div));
+                rp[idx] = -RK_P_FACTOR * rho[idx] * div;
+            }
+}
+
+/* periodic copies of u,v,w,p,rho,T: x faces, y faces, z faces */
+static void rk_apply_periodic(flow_field* f) {
+    double* a[6] = {f->u, f->v, f->w, f->p, f->rho, f->T};
+    for (int q = 0; q < 6; q++)
+        if (a[q]) oracle_bc_periodic_3d(a[q], f->nx, f->ny, f->nz);
+}
+
+cfd_status_t oracle_rk4_step(flow_field* field, const grid* grid, const ns_solver_params_t* params,
+                             ns_solver_stats_t* stats) {
+    if (field->nx < 3 || field->ny < 3 || (field->nz > 1 && field->nz < 3)) return CFD_ERROR_INVALID;
+    size_t nx = field->nx, ny = field->ny, nz = field->nz;
+    if (nz > 1 && grid->dz)
+        for (size_t k = 1; k < nz - 1; k++)
+            if (fabs(grid->dz[k] - grid->dz[0]) > 1e-14) return CFD_ERROR_INVALID;
+    size_t total = nx * ny * nz, bytes = total * sizeof(double);
+    double* buf = (double*)calloc(20 * total, sizeof(double));
+    if (!buf) return CFD_ERROR_NOMEM;
+    double* K[4][4];
+    for (int s = 0; s < 4; s++)
+        for (int q = 0; q < 4; q++) K[s][q] = buf + (size_t)(s * 4 + q) * total;
+    double* Q0[4];
+    for (int q = 0; q < 4; q++) Q0[q] = buf + (size_t)(16 + q) * total;
+    double* F[4] = {field->u, field->v, field->w, field->p};
+    const double dt = params->dt;
+    const int iter = 0; /* rk4_step forces max_iter = 1 (solver_registry.c:756-759) */
+    for (int q = 0; q < 4; q++) memcpy(Q0[q], F[q], bytes);
+    const double fac[3] = {0.5 * dt, 0.5 * dt, dt};
+    for (int s = 0; s < 4; s++) {
+        rk_rhs(field, grid, params, K[s][0], K[s][1], K[s][2], K[s][3], iter, dt);
+        if (s == 3) break;
+        /* apply_stage_update (solver_rk4.c:47-63) */
+        for (size_t n = 0; n < total; n++) {
+            for (int q = 0; q < 4; q++) F[q][n] = Q0[q][n] + fac[s] * K[s][q][n];
+            for (int q = 0; q < 3; q++) F[q][n] = clampv(F[q][n]);
+        }
+    }
+    double sixth_dt = dt / 6.0;
+    for (size_t n = 0; n < total; n++) {
+        for (int q = 0; q < 4; q++)
+            F[q][n] = Q0[q][n] + sixth_dt * (K[0][q][n] + 2.0 * K[1][q][n] + 2.0 * K[2][q][n] +
+                                             K[3][q][n]);
+        for (int q = 0; q < 3; q++) F[q][n] = clampv(F[q][n]);
+    }
+    free(buf);
+    cfd_status_t st = oracle_energy_step(field, grid, params, dt, iter * dt);
+    if (st != CFD_SUCCESS) return st;
+    rk_apply_periodic(field);
+    st = oracle_apply_thermal_bcs(field, params);
+    if (st != CFD_SUCCESS) return st;
+    for (size_t n = 0; n < total; n++)
+        if (!isfinite(field->u[n]) || !isfinite(field->v[n]) || !isfinite(field->w[n]) ||
+            !isfinite(field->p[n]))
+            return CFD_ERROR_DIVERGED;
+    if (stats) {
+        stats->iterations = 1;
+        oracle_max_velocity_pressure(field, &stats->max_velocity, &stats->max_pressure);
+        stats->max_temperature = oracle_max_temperature(field);
+    }
+    return CFD_SUCCESS;
+}

@@ -109,6 +109,11 @@ cfd_status_t oracle_energy_step(flow_field* field, const grid* g, const ns_solve
                                 double dt, double time);
 cfd_status_t oracle_apply_thermal_bcs(flow_field* field, const ns_solver_params_t* params);
 
+/* One RK4 step as rk4_step (solver_registry.c:748-772) -> rk4_impl
+ * (solver_rk4.c:69-259) with max_iter = 1. */
+cfd_status_t oracle_rk4_step(flow_field* field, const grid* g, const ns_solver_params_t* params,
+                             ns_solver_stats_t* stats);
+
 /* solver_registry.c:31-62 */
 void oracle_max_velocity_pressure(const flow_field* f, double* max_vel, double* max_p);
 double oracle_max_temperature(const flow_field* f);

@@ -70,6 +70,8 @@ def lib():
         sig("oracle_params_default", A.SolverParams)
         sig("oracle_max_velocity_pressure", None, P(A.FlowField), d, d)
         sig("oracle_apply_thermal_bcs", C.c_int, P(A.FlowField), P(A.SolverParams))
+        sig("oracle_rk4_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
+            P(A.SolverStats))
         sig("oracle_energy_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
             C.c_double, C.c_double)
         _lib = L
@@ -140,6 +142,13 @@ def jacobi_solve(x, rhs, dx, dy, dz, params=None):
 def cg_fixed_iters(x, rhs, dx, dy, dz, iters) -> float:
     nz, ny, nx = x.shape
     return lib().oracle_cg_fixed_iters(_dp(x), _dp(rhs), nx, ny, nz, dx, dy, dz, iters)
+
+
+def rk4_step(field, grid, params):
+    """rk4_step -> rk4_impl (solver_rk4.c:69-259), one step; returns (status, stats)."""
+    st = A.SolverStats()
+    s = lib().oracle_rk4_step(field.ptr, grid.ptr, C.byref(params), C.byref(st))
+    return s, st
 
 
 def apply_thermal_bcs(field, params) -> int:

@@ -14,6 +14,8 @@ from cfd_amd import api
 
 # tests/solvers/navier_stokes/cpu/test_ns_solver_3d.c:345-348 (projection, nz = 1)
 KAT_PROJECTION_L2 = (6.84647639323831686e-02, 3.42315494726977212e-02, 1.00000039251590289e+00)
+# test_ns_solver_3d.c:363-366 (RK4, nz = 1; one step: the step wrapper forces max_iter = 1)
+KAT_RK4_L2 = (6.88584742267390471e-02, 3.49775875752817156e-02, 1.00000000000000000e+00)
 
 
 def kat_2d():

@@ -21,6 +21,16 @@ def test_projection_kat_bitexact():
     assert st.iterations == 1 and iters > 0
 
 
+def test_rk4_kat_bitexact():
+    """test_ns_solver_3d.c:363-366 RK4 golden L2 triple, bit for bit."""
+    g, f, p = cases.kat_2d()
+    s, st = oracle.rk4_step(f, g, p)
+    assert s == A.CFD_SUCCESS and st.iterations == 1
+    l2 = (cases.l2_rms(f.u), cases.l2_rms(f.v), cases.l2_rms(f.p))
+    assert l2 == cases.KAT_RK4_L2
+    assert np.all(f.w == 0.0)
+
+
 @pytest.mark.parametrize("n,expected", [(33, 47), (65, 97)])
 def test_cg_iteration_counts(n, expected):
     """CG cold solve on the cos*cos*cos rhs: 47 / 97 iterations at 33^3 / 65^3
