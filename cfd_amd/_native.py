@@ -141,7 +141,11 @@ def _bind_hip(lib) -> None:
          P(A.HipProjConfig))
     _sig(lib, "hip_proj_slab_info", C.c_int, V, P(C.c_size_t), P(C.c_size_t), P(C.c_int),
          P(C.c_int))
+    _sig(lib, "hip_rk4_step_device", C.c_int, V, P(A.Grid), P(A.SolverParams), P(A.SolverStats))
+    _sig(lib, "hip_rk4_step", C.c_int, V, P(A.FlowField), P(A.Grid), P(A.SolverParams),
+         P(A.SolverStats))
     _sig(lib, "create_projection_hip_solver", P(A.NSSolver))
+    _sig(lib, "create_rk4_hip_solver", P(A.NSSolver))
     _sig(lib, "cfd_hip_register_solvers", None, V)
 
 

@@ -78,6 +78,9 @@ struct hip_proj_ctx {
     double *r = nullptr, *pa = nullptr, *pb = nullptr;
     double *rhs = nullptr, *xt = nullptr;
     double* Tn = nullptr;  // energy equation output (swapped with T)
+    double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated
+    double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3
+    double *dxa = nullptr, *dya = nullptr;  // grid->dx[], grid->dy[] (RK4 per-index spacing)
     double *src_u_row = nullptr, *src_v_col = nullptr;
     std::vector<double> h_src_u, h_src_v;
     // reductions / state
@@ -132,6 +135,7 @@ static double* field_ptr(hip_proj_ctx* c, int id) {
         case HIP_FIELD_W: return c->w;
         case HIP_FIELD_P: return c->p;
         case HIP_FIELD_T: return c->T;
+        case HIP_FIELD_RHO: return c->rho;
         default: return nullptr;
     }
 }
@@ -269,10 +273,10 @@ static const unsigned long long* reduce_red(hip_proj_ctx* c, cfd_status_t* st) {
 // Shared by the integrators (defined in projection_hip.hip).
 cfd_status_t ctx_apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t& t, bool is3d)
     __attribute__((visibility("hidden")));
-// Energy equation on the current velocity + thermal BCs (alpha > 0 only);
-// sets red[5] on non-finite T.
-cfd_status_t ctx_energy_step(hip_proj_ctx* c, const grid* g, const ns_solver_params_t* prm)
-    __attribute__((visibility("hidden")));
+// Energy equation on the current velocity (alpha > 0 only), then the thermal
+// BCs when apply_bcs; sets red[5] on non-finite T.
+cfd_status_t ctx_energy_step(hip_proj_ctx* c, const grid* g, const ns_solver_params_t* prm,
+                             bool apply_bcs) __attribute__((visibility("hidden")));
 // Field validation shared by the step functions (grid match, callbacks,
 // thermal BC types).
 cfd_status_t ctx_validate_params(const hip_proj_ctx* c, const grid* g,

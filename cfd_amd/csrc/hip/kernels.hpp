@@ -985,6 +985,166 @@ static __global__ __launch_bounds__(256) void k_thermal_bc(Geo g, double* __rest
 }
 
 // ---------------------------------------------------------------------------
+// RK4 (solver_rk4.c:69-259) with the shared momentum RHS
+// (ns_momentum_rhs_scalar.h:49-190). One fused kernel per stage s:
+//   k      = RHS(cur)                      (interior; 0 on boundary cells)
+//   acc    = k | acc + 2k | acc + 2k       (s = 0, 1, 2: the reference's
+//                                           k1 + 2 k2 + 2 k3 + k4, left to right)
+//   out    = clamp(Q0 + fac_s k)           (s < 3; fac = dt/2, dt/2, dt)
+//   out    = clamp(Q0 + dt/6 (acc + k))    (s = 3, written in place over Q0)
+// so the stage derivatives never touch HBM. The stencil uses the
+// reference's periodic neighbour indices (i = 1 reads nx-2, not the ghost).
+// ---------------------------------------------------------------------------
+struct RkCoef {
+    double inv_2dz, inv_dz2;
+    double mu, beta, T_ref, g0, g1, g2;
+    double fac;   // dt/2, dt/2, dt, dt/6
+};
+
+struct Fld4 {
+    double* f[4];  // u, v, w, p
+};
+
+__device__ __forceinline__ double clampl(double x, double lim) { return fmax(-lim, fmin(lim, x)); }
+
+template <int STAGE, bool BUOY>
+__global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
+                                                  Fld4 out, const double* __restrict__ rho,
+                                                  const double* __restrict__ T,
+                                                  const double* __restrict__ dxa,
+                                                  const double* __restrict__ dya,
+                                                  const double* __restrict__ su_row,
+                                                  const double* __restrict__ sv_col) {
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    if (i >= g.nx || j >= g.ny) return;
+    const long long idx = cidx(g, i, j, k);
+    const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
+                           k >= g.k0 && k < g.k1);
+    double kr[4] = {0.0, 0.0, 0.0, 0.0};
+    if (interior) {
+        const double r = rho[idx];
+        const double dxi = dxa[i], dyj = dya[j];
+        if (!(r <= 1e-10) && !(fabs(dxi) < 1e-10) && !(fabs(dyj) < 1e-10)) {
+            const long long il = (i > 1) ? idx - 1 : cidx(g, g.nx - 2, j, k);
+            const long long ir = (i < g.nx - 2) ? idx + 1 : cidx(g, 1, j, k);
+            const long long jd = (j > 1) ? idx - g.px : cidx(g, i, g.ny - 2, k);
+            const long long ju = (j < g.ny - 2) ? idx + g.px : cidx(g, i, 1, k);
+            long long kd = idx, ku = idx;   // 2-D: z terms vanish (stride 0)
+            if (g.sz) {
+                kd = (k > 1) ? idx - g.sz : cidx(g, i, j, g.nz - 2);
+                ku = (k < g.nz - 2) ? idx + g.sz : cidx(g, i, j, 1);
+            }
+            const double* U = cur.f[0];
+            const double* V = cur.f[1];
+            const double* W = cur.f[2];
+            const double* P = cur.f[3];
+            const double tdx = 2.0 * dxi, tdy = 2.0 * dyj;
+            const double dxx = dxi * dxi, dyy = dyj * dyj;
+            const double uc = U[idx], vc = V[idx], wc = W[idx];
+            double du_dx = (U[ir] - U[il]) / tdx, du_dy = (U[ju] - U[jd]) / tdy;
+            double du_dz = (U[ku] - U[kd]) * rc.inv_2dz;
+            double dv_dx = (V[ir] - V[il]) / tdx, dv_dy = (V[ju] - V[jd]) / tdy;
+            double dv_dz = (V[ku] - V[kd]) * rc.inv_2dz;
+            double dw_dx = (W[ir] - W[il]) / tdx, dw_dy = (W[ju] - W[jd]) / tdy;
+            double dw_dz = (W[ku] - W[kd]) * rc.inv_2dz;
+            double dp_dx = (P[ir] - P[il]) / tdx, dp_dy = (P[ju] - P[jd]) / tdy;
+            double dp_dz = (P[ku] - P[kd]) * rc.inv_2dz;
+            double d2u_dx2 = (U[ir] - 2.0 * uc + U[il]) / dxx;
+            double d2u_dy2 = (U[ju] - 2.0 * uc + U[jd]) / dyy;
+            double d2u_dz2 = (U[ku] - 2.0 * uc + U[kd]) * rc.inv_dz2;
+            double d2v_dx2 = (V[ir] - 2.0 * vc + V[il]) / dxx;
+            double d2v_dy2 = (V[ju] - 2.0 * vc + V[jd]) / dyy;
+            double d2v_dz2 = (V[ku] - 2.0 * vc + V[kd]) * rc.inv_dz2;
+            double d2w_dx2 = (W[ir] - 2.0 * wc + W[il]) / dxx;
+            double d2w_dy2 = (W[ju] - 2.0 * wc + W[jd]) / dyy;
+            double d2w_dz2 = (W[ku] - 2.0 * wc + W[kd]) * rc.inv_dz2;
+            double nu = rc.mu / fmax(r, 1e-10);
+            nu = fmin(nu, 1.0);
+            du_dx = clampl(du_dx, 100.0); du_dy = clampl(du_dy, 100.0); du_dz = clampl(du_dz, 100.0);
+            dv_dx = clampl(dv_dx, 100.0); dv_dy = clampl(dv_dy, 100.0); dv_dz = clampl(dv_dz, 100.0);
+            dw_dx = clampl(dw_dx, 100.0); dw_dy = clampl(dw_dy, 100.0); dw_dz = clampl(dw_dz, 100.0);
+            dp_dx = clampl(dp_dx, 100.0); dp_dy = clampl(dp_dy, 100.0); dp_dz = clampl(dp_dz, 100.0);
+            d2u_dx2 = clampl(d2u_dx2, 1000.0); d2u_dy2 = clampl(d2u_dy2, 1000.0);
+            d2u_dz2 = clampl(d2u_dz2, 1000.0); d2v_dx2 = clampl(d2v_dx2, 1000.0);
+            d2v_dy2 = clampl(d2v_dy2, 1000.0); d2v_dz2 = clampl(d2v_dz2, 1000.0);
+            d2w_dx2 = clampl(d2w_dx2, 1000.0); d2w_dy2 = clampl(d2w_dy2, 1000.0);
+            d2w_dz2 = clampl(d2w_dz2, 1000.0);
+            double su = su_row[j], sv = sv_col[i], sw = 0.0;
+            if (BUOY) {
+                const double dT = T[idx] - rc.T_ref;
+                su += -rc.beta * dT * rc.g0;
+                sv += -rc.beta * dT * rc.g1;
+                sw += -rc.beta * dT * rc.g2;
+            }
+            kr[0] = -uc * du_dx - vc * du_dy - wc * du_dz - dp_dx / r +
+                    nu * (d2u_dx2 + d2u_dy2 + d2u_dz2) + su;
+            kr[1] = -uc * dv_dx - vc * dv_dy - wc * dv_dz - dp_dy / r +
+                    nu * (d2v_dx2 + d2v_dy2 + d2v_dz2) + sv;
+            kr[2] = -uc * dw_dx - vc * dw_dy - wc * dw_dz - dp_dz / r +
+                    nu * (d2w_dx2 + d2w_dy2 + d2w_dz2) + sw;
+            double div = du_dx + dv_dy + dw_dz;
+            div = fmax(-10.0, fmin(10.0, div));
+            kr[3] = -0.1 * r * div;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double o;
+        if (STAGE == 0) {
+            acc.f[q][idx] = kr[q];
+            o = q0.f[q][idx] + rc.fac * kr[q];
+        } else if (STAGE < 3) {
+            acc.f[q][idx] = acc.f[q][idx] + 2.0 * kr[q];
+            o = q0.f[q][idx] + rc.fac * kr[q];
+        } else {
+            o = q0.f[q][idx] + rc.fac * (acc.f[q][idx] + kr[q]);
+        }
+        if (q < 3) o = fmax(-100.0, fmin(100.0, o));
+        out.f[q][idx] = o;
+    }
+}
+
+// max |u|, max |p| and the non-finite flag over the owned planes (the
+// stats / NaN scan of the RK wrappers, solver_registry.c:31-49,760-768)
+static __global__ __launch_bounds__(256) void k_vel_stats(Geo g, const double* __restrict__ U,
+                                                          const double* __restrict__ V,
+                                                          const double* __restrict__ W,
+                                                          const double* __restrict__ P,
+                                                          unsigned long long* red) {
+    __shared__ double shv[4], shp[4];
+    __shared__ int shbad;
+    if (threadIdx.x == 0) shbad = 0;
+    __syncthreads();
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    double mv = 0.0, mp = 0.0;
+    if (i < g.nx && j < g.ny) {
+        const long long idx = cidx(g, i, j, k);
+        const double u = U[idx], v = V[idx], w = W[idx], p = P[idx];
+        if (!isfinite(u) || !isfinite(v) || !isfinite(w) || !isfinite(p)) shbad = 1;
+        const double vel = sqrt((u * u) + (v * v) + (w * w));
+        if (vel > mv) mv = vel;
+        const double ap = fabs(p);
+        if (ap > mp) mp = ap;
+    }
+    mv = wave_max(mv);
+    mp = wave_max(mp);
+    if ((threadIdx.x & 63) == 0) {
+        shv[threadIdx.x >> 6] = mv;
+        shp[threadIdx.x >> 6] = mp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicMax(&red[0], ord_enc(fmax(fmax(shv[0], shv[1]), fmax(shv[2], shv[3]))));
+        atomicMax(&red[1], ord_enc(fmax(fmax(shp[0], shp[1]), fmax(shp[2], shp[3]))));
+        if (shbad) atomicOr(&red[2], 1ull);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Relaxation solvers.
 // Red-Black SOR colour pass (linear_solver_redblack.c:97-133). `parity` is the
 // (i+j+k) parity updated in this pass: the reference's first ("red") pass

@@ -585,9 +585,10 @@ cfd_status_t hip_proj_synchronize(hip_proj_ctx_t* c) {
 cfd_status_t hip_proj_set_field(hip_proj_ctx_t* c, int id, const double* host) {
     if (!c || !host) return CFD_ERROR_INVALID;
     double* d = field_ptr(c, id);
-    if (id == HIP_FIELD_T && !d) {
-        if (dalloc(c, &c->T, field_elems(c)) != CFD_SUCCESS) return CFD_ERROR_NOMEM;
-        d = c->T;
+    if ((id == HIP_FIELD_T || id == HIP_FIELD_RHO) && !d) {
+        double** slot = (id == HIP_FIELD_T) ? &c->T : &c->rho;
+        if (dalloc(c, slot, field_elems(c)) != CFD_SUCCESS) return CFD_ERROR_NOMEM;
+        d = *slot;
     }
     if (!d) return CFD_ERROR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
@@ -620,10 +621,11 @@ static __global__ void k_fill(double* f, long long n, double v) {
 cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
     if (!c) return CFD_ERROR_INVALID;
     double* d = field_ptr(c, id);
-    if (id == HIP_FIELD_T && !d) {
-        if (dalloc(c, &c->T, field_elems(c)) != CFD_SUCCESS) return CFD_ERROR_NOMEM;
-        d = c->T;
-        c->have_T = 1;
+    if ((id == HIP_FIELD_T || id == HIP_FIELD_RHO) && !d) {
+        double** slot = (id == HIP_FIELD_T) ? &c->T : &c->rho;
+        if (dalloc(c, slot, field_elems(c)) != CFD_SUCCESS) return CFD_ERROR_NOMEM;
+        d = *slot;
+        if (id == HIP_FIELD_T) c->have_T = 1;
     }
     if (!d) return CFD_ERROR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
@@ -780,7 +782,8 @@ cfd_status_t ctx_apply_thermal_bcs(hip_proj_ctx* c, const ns_thermal_bc_config_t
     return CFD_SUCCESS;
 }
 
-cfd_status_t ctx_energy_step(hip_proj_ctx* c, const grid* g, const ns_solver_params_t* prm) {
+cfd_status_t ctx_energy_step(hip_proj_ctx* c, const grid* g, const ns_solver_params_t* prm,
+                             bool apply_bcs) {
     // energy_step_explicit_with_workspace (energy_solver.c:21-176) on the
     // current velocity, then energy_apply_thermal_bcs (:204-334)
     const size_t nz = c->nzg;
@@ -801,7 +804,7 @@ cfd_status_t ctx_energy_step(hip_proj_ctx* c, const grid* g, const ns_solver_par
                               c->geo, ec, c->T, c->u, c->v, c->w, c->Tn, c->red);
     });
     std::swap(c->T, c->Tn);
-    ST_TRY(ctx_apply_thermal_bcs(c, prm->thermal_bc, nz > 1));
+    if (apply_bcs) ST_TRY(ctx_apply_thermal_bcs(c, prm->thermal_bc, nz > 1));
     c->T_dirty = 1;
     return CFD_SUCCESS;
 }
@@ -931,7 +934,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                            c->ws, c->pn, c->u, c->v, c->w, c->red);
     });
     std::swap(c->p, c->pn);  // memcpy(field->p, p_new) (solver_projection.c:253)
-    if (energy) ST_TRY(ctx_energy_step(c, g, prm));  // solver_projection.c:255-274
+    if (energy) ST_TRY(ctx_energy_step(c, g, prm, true));  // solver_projection.c:255-274
     ctx_queue_max_T(c);
     const unsigned long long* red = reduce_red(c, &s);
     if (s != CFD_SUCCESS) return s;

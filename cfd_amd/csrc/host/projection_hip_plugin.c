@@ -27,6 +27,10 @@ CFD_HIP_INTERNAL cfd_status_t hip_proj_step_iter_internal(hip_proj_ctx_t* ctx, f
                                                           const grid* g,
                                                           const ns_solver_params_t* params,
                                                           ns_solver_stats_t* stats, int n_steps);
+CFD_HIP_INTERNAL cfd_status_t hip_rk4_step_iter_internal(hip_proj_ctx_t* ctx, flow_field* field,
+                                                         const grid* g,
+                                                         const ns_solver_params_t* params,
+                                                         ns_solver_stats_t* stats, int n_steps);
 CFD_HIP_INTERNAL int hip_proj_matches_internal(const hip_proj_ctx_t* ctx, size_t nx, size_t ny,
                                                size_t nz);
 
@@ -88,6 +92,18 @@ static void plugin_destroy(ns_solver_t* solver) {
     }
 }
 
+static int is_rk4(const ns_solver_t* solver) {
+    return solver->name && strcmp(solver->name, NS_SOLVER_TYPE_RK4_HIP) == 0;
+}
+
+/* n steps of the solver's integrator on host buffers */
+static cfd_status_t run_steps(ns_solver_t* solver, hip_proj_ctx_t* ctx, flow_field* field,
+                              const grid* g, const ns_solver_params_t* params,
+                              ns_solver_stats_t* stats, int n) {
+    if (is_rk4(solver)) return hip_rk4_step_iter_internal(ctx, field, g, params, stats, n);
+    return hip_proj_step_iter_internal(ctx, field, g, params, stats, n);
+}
+
 static cfd_status_t plugin_step(ns_solver_t* solver, flow_field* field, const grid* g,
                                 const ns_solver_params_t* params, ns_solver_stats_t* stats) {
     if (!field || !g || !params) return CFD_ERROR_INVALID;
@@ -95,7 +111,7 @@ static cfd_status_t plugin_step(ns_solver_t* solver, flow_field* field, const gr
     hip_proj_ctx_t* ctx = NULL;
     cfd_status_t s = get_ctx(solver, g, &ctx);
     if (s != CFD_SUCCESS) return s;
-    return hip_proj_step_iter_internal(ctx, field, g, params, stats, 1);
+    return run_steps(solver, ctx, field, g, params, stats, 1);
 }
 
 static cfd_status_t plugin_solve(ns_solver_t* solver, flow_field* field, const grid* g,
@@ -105,7 +121,7 @@ static cfd_status_t plugin_solve(ns_solver_t* solver, flow_field* field, const g
     hip_proj_ctx_t* ctx = NULL;
     cfd_status_t s = get_ctx(solver, g, &ctx);
     if (s != CFD_SUCCESS) return s;
-    s = hip_proj_step_iter_internal(ctx, field, g, params, stats, params->max_iter);
+    s = run_steps(solver, ctx, field, g, params, stats, params->max_iter);
     if (s == CFD_SUCCESS && stats) stats->iterations = params->max_iter;
     return s;
 }
@@ -146,6 +162,11 @@ ns_solver_t* create_projection_hip_jacobi_solver(void) {
                        "Projection method with Jacobi pressure solve (HIP, MI355X)");
 }
 
+/* rk4_hip: rk4_step / rk4_solve (solver_registry.c:748-800) on the device */
+ns_solver_t* create_rk4_hip_solver(void) {
+    return make_solver(NS_SOLVER_TYPE_RK4_HIP, "RK4 time integration (HIP, MI355X)");
+}
+
 void cfd_hip_register_solvers(ns_solver_registry_t* registry) {
     if (!registry || !cfd_registry_register) return;
     cfd_registry_register(registry, NS_SOLVER_TYPE_PROJECTION_HIP, create_projection_hip_solver);
@@ -153,4 +174,5 @@ void cfd_hip_register_solvers(ns_solver_registry_t* registry) {
                           create_projection_hip_rbsor_solver);
     cfd_registry_register(registry, NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI,
                           create_projection_hip_jacobi_solver);
+    cfd_registry_register(registry, NS_SOLVER_TYPE_RK4_HIP, create_rk4_hip_solver);
 }

@@ -35,6 +35,7 @@ extern "C" {
 #define NS_SOLVER_TYPE_PROJECTION_HIP        "projection_hip"
 #define NS_SOLVER_TYPE_PROJECTION_HIP_RBSOR  "projection_hip_rbsor"
 #define NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI "projection_hip_jacobi"
+#define NS_SOLVER_TYPE_RK4_HIP               "rk4_hip"
 
 /* Pressure-Poisson method used inside the HIP projection step. */
 typedef enum {
@@ -70,7 +71,8 @@ typedef enum {
     HIP_FIELD_V = 1,
     HIP_FIELD_W = 2,
     HIP_FIELD_P = 3,
-    HIP_FIELD_T = 4
+    HIP_FIELD_T = 4,
+    HIP_FIELD_RHO = 5  /* per-cell density (read by RK4; the projection uses rho[0]) */
 } hip_field_id_t;
 
 /* Per-kernel timing (filled when profiling is enabled). */
@@ -83,7 +85,8 @@ typedef enum {
     HIP_KT_RELAX = 5,      /* one RB-SOR colour pass or one Jacobi sweep */
     HIP_KT_RESIDUAL = 6,   /* L-infinity residual for the relaxation methods */
     HIP_KT_ENERGY = 7,     /* energy equation (alpha > 0) */
-    HIP_KT_COUNT = 8
+    HIP_KT_RK_STAGE = 8,   /* one fused RK4 stage (RHS + stage update) */
+    HIP_KT_COUNT = 9
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);
@@ -208,11 +211,27 @@ CFD_HIP_EXPORT hip_proj_ctx_t* hip_proj_create_slab(size_t nx, size_t ny, size_t
 CFD_HIP_EXPORT cfd_status_t hip_proj_slab_info(const hip_proj_ctx_t* ctx, size_t* k_offset,
                                                size_t* nz_local, int* rank, int* size);
 
+/* ---- RK4 (solver_rk4.c:69-259) --------------------------------------------
+ * Classical RK4 with the shared momentum RHS of ns_momentum_rhs_scalar.h:49-190
+ * (periodic stencil indices, derivative clamps, pseudo-compressible pressure
+ * update), energy equation after the update, periodic BCs on u,v,w,p,rho,T,
+ * thermal BCs, NaN check: the reference `rk4` step on a context's fields. The
+ * context needs HIP_FIELD_RHO (per-cell density) in addition to u,v,w,p (T when
+ * beta != 0 or alpha > 0). Single device only. */
+CFD_HIP_EXPORT cfd_status_t hip_rk4_step_device(hip_proj_ctx_t* ctx, const grid* g,
+                                                const ns_solver_params_t* params,
+                                                ns_solver_stats_t* stats);
+/* Host-buffer step: upload u,v,w,p,rho(,T), one RK4 step, download. */
+CFD_HIP_EXPORT cfd_status_t hip_rk4_step(hip_proj_ctx_t* ctx, flow_field* field, const grid* g,
+                                         const ns_solver_params_t* params,
+                                         ns_solver_stats_t* stats);
+
 /* ---- plugin surface ------------------------------------------------------ */
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_rbsor_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_jacobi_solver(void);
-/* Registers the three names above through cfd_registry_register(). */
+CFD_HIP_EXPORT ns_solver_t* create_rk4_hip_solver(void);
+/* Registers the four names above through cfd_registry_register(). */
 CFD_HIP_EXPORT void cfd_hip_register_solvers(ns_solver_registry_t* registry);
 
 #ifdef __cplusplus
