@@ -41,10 +41,11 @@ static void launch_cgB_f(hip_proj_ctx* c, const Lap& L, const double* p, double*
     dist(c) ? launch_cgB_t<TY, true, FL>(c, L, p, r, it) : launch_cgB_t<TY, false, FL>(c, L, p, r, it);
 }
 
-// sweep_ty 4 or 8; sweep_variant selects the SW_NT_* flags (TY 8 only)
+// sweep_ty 4, 8 or 16; sweep_variant selects the SW_NT_* flags (TY 8 only)
 static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
                        const double* po, double* pn, double* x, int it) {
     if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, x, it);
+    if (c->sweep_ty == 16) return launch_cgA_f<16, 0>(c, first, L, r, po, pn, x, it);
     switch (c->sweep_variant) {
         case 1: return launch_cgA_f<8, 1>(c, first, L, r, po, pn, x, it);
         case 2: return launch_cgA_f<8, 2>(c, first, L, r, po, pn, x, it);
@@ -55,6 +56,7 @@ static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* 
 
 static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
     if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, L, p, r, it);
+    if (c->sweep_ty == 16) return launch_cgB_f<16, 0>(c, L, p, r, it);
     switch (c->sweep_variant) {
         case 1: return launch_cgB_f<8, 1>(c, L, p, r, it);
         case 2: return launch_cgB_f<8, 2>(c, L, p, r, it);
@@ -432,7 +434,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     g.tiles_z = (nint_k + g.kc - 1) / g.kc;
 
     // row-pair CG sweeps: 128 x TY x kc tiles (kernels.hpp, k_cgA / k_cgB)
-    c->sweep_ty = (c->cfg.sweep_rows == 4) ? 4 : 8;
+    c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
     c->sweep_variant = c->cfg.sweep_variant & 3;
     SGeo& sg = c->sgeo;
     sg.nx = g.nx;

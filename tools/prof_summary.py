@@ -33,13 +33,37 @@ def stats(path: Path):
 
 
 def pmc(path: Path):
+    """Mean counter value per kernel over the dispatches that did work: CG
+    sweeps launched ahead of the host's convergence poll return at once after
+    convergence and report ~0; they are left out (< 1 % of the kernel's max)."""
     acc = defaultdict(list)
     if not path.exists():
         return {}
     with open(path) as f:
         for row in csv.DictReader(f):
             acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    out = {}
+    for k, v in acc.items():
+        big = [x for x in v if x > 0.01 * max(v)] or v
+        out[k] = sum(big) / len(big)
+    return out
+
+
+def trace_real(path: Path):
+    """Mean duration (us) per kernel over dispatches longer than 1 % of the
+    kernel's longest (the same no-op filter), from the kernel trace."""
+    acc = defaultdict(list)
+    if not path.exists():
+        return {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            acc[short(row["Kernel_Name"])].append(
+                (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
+    out = {}
+    for k, v in acc.items():
+        big = [x for x in v if x > 0.01 * max(v)] or v
+        out[k] = (len(big), sum(big) / len(big))
+    return out
 
 
 def main():
@@ -48,18 +72,21 @@ def main():
     if "--cells" in sys.argv:
         cells = float(sys.argv[sys.argv.index("--cells") + 1])
     st = stats(d / "trace" / "run_kernel_stats.csv")
+    real = trace_real(d / "trace" / "run_kernel_trace.csv")
     fe = pmc(d / "fetch" / "run_counter_collection.csv")
     wr = pmc(d / "write" / "run_counter_collection.csv")
-    print(f"{'kernel':34s} {'calls':>6s} {'avg_us':>10s} {'total_ms':>10s} "
-          f"{'FETCH_KB':>12s} {'WRITE_KB':>12s}" + ("  B/cell(fetch,write)" if cells else ""))
+    print(f"{'kernel':34s} {'calls':>6s} {'avg_us':>10s} {'work_n':>6s} {'work_us':>10s} "
+          f"{'total_ms':>10s} {'FETCH_KB':>12s} {'WRITE_KB':>12s}"
+          + ("  B/cell(2*fetch,write)" if cells else ""))
     for k, (n, avg, tot) in sorted(st.items(), key=lambda kv: -kv[1][2]):
         f = fe.get(k)
         w = wr.get(k)
-        line = f"{k:34s} {n:6d} {avg:10.2f} {tot:10.2f} " \
+        rn, ravg = real.get(k, (n, avg))
+        line = f"{k:34s} {n:6d} {avg:10.2f} {rn:6d} {ravg:10.2f} {tot:10.2f} " \
                f"{(f'{f:12.0f}' if f is not None else ' ' * 12)} " \
                f"{(f'{w:12.0f}' if w is not None else ' ' * 12)}"
         if cells and (f is not None or w is not None):
-            fb = f * 1024 / cells if f is not None else float("nan")
+            fb = 2 * f * 1024 / cells if f is not None else float("nan")
             wb = w * 1024 / cells if w is not None else float("nan")
             line += f"  {fb:6.2f},{wb:6.2f}"
         print(line)
@@ -68,7 +95,8 @@ def main():
         out = {}
         for k, (n, avg, tot) in st.items():
             f, w = fe.get(k), wr.get(k)
-            rec = {"calls": n, "avg_us": avg}
+            rn, ravg = real.get(k, (n, avg))
+            rec = {"calls": n, "avg_us": avg, "working_calls": rn, "working_avg_us": ravg}
             if f is not None and w is not None:
                 rec["fetch_size_kb"] = f
                 rec["write_size_kb"] = w
