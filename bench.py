@@ -31,6 +31,10 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# rocprofv3 PMC summary of this workload (tools/gpu_profile.sh + prof_summary.py):
+# 2*FETCH_SIZE + WRITE_SIZE per working launch of sweep A, the gfx950
+# correction of MI355X_MICROARCH.md "HBM [CDNA4]".
+TRAFFIC_JSON = ROOT / "profiles" / "r01_traffic_cg_sweeps.json"
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 40.0    # read r, p_old, x; write p_new, x
 BYTES_SWEEP_B = 24.0    # read p, r; write r
@@ -146,6 +150,8 @@ def main():
     cg_iter_ms = avg_a + avg_b
     cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_loc / (cg_iter_ms * 1e-3) / 1e9
 
+    traffic, traffic_src = pmc_traffic("k_cgA<", n_loc) if world == 1 else (None, None)
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n, args, k_mean)
@@ -177,7 +183,9 @@ def main():
                          "achieved": round(ach_a, 1) if ach_a else None,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach_a / HBM_PEAK_GBPS, 4) if ach_a else None,
-                         "traffic": None, "bytes_per_cell": BYTES_SWEEP_A,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes": BYTES_SWEEP_A * n_loc,
+                         "bytes_per_cell": BYTES_SWEEP_A,
                          "avg_launch_ms": round(avg_a, 4)},
             "kernels": {k: {"total_ms": round(v[0], 3), "launches": v[1],
                             "avg_ms": round(v[0] / v[1], 4) if v[1] else None}
@@ -192,6 +200,21 @@ def main():
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(prefix, cells):
+    """HBM bytes per launch of the kernel from the committed PMC summary, if it
+    was recorded for this grid size (else None)."""
+    try:
+        d = json.loads(TRAFFIC_JSON.read_text())
+    except (OSError, ValueError):
+        return None, None
+    if d.get("cells_per_launch") != float(cells):
+        return None, None
+    for k, v in d.get("kernels", {}).items():
+        if k.startswith(prefix) and "true" not in k and "hbm_bytes_per_launch" in v:
+            return round(v["hbm_bytes_per_launch"]), f"{TRAFFIC_JSON.name}: {k}"
+    return None, None
 
 
 def cpu_baseline(n, args, k_gpu):
