@@ -34,7 +34,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh + prof_summary.py):
 # 2*FETCH_SIZE + WRITE_SIZE per working launch of sweep A, the gfx950
 # correction of MI355X_MICROARCH.md "HBM [CDNA4]".
-TRAFFIC_JSON = ROOT / "profiles" / "r01_traffic_cg_sweeps.json"
+TRAFFIC_JSON = ROOT / "profiles" / "r01b_traffic_cg_sweeps.json"
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 40.0    # read r, p_old, x; write p_new, x
 BYTES_SWEEP_B = 24.0    # read p, r; write r
@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--cpu-cg-iters", type=int, default=100,
                     help="CG iterations timed in the CPU baseline sample")
     ap.add_argument("--kchunk", type=int, default=0)
-    ap.add_argument("--sweep-rows", type=int, default=8)
+    ap.add_argument("--sweep-rows", type=int, default=16)
+    ap.add_argument("--sweep-variant", type=int, default=3,
+                    help="CG sweep memory hints: 1 NT stores, 2 NT loads, 3 both")
     return ap.parse_args()
 
 
@@ -91,7 +93,7 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = api.SlabComm.rccl(uid[0], rank, world, local)
     ctx = api.HipProjection(n, n, n, comm=comm, device=local, kchunk=args.kchunk,
-                             sweep_rows=args.sweep_rows)
+                             sweep_rows=args.sweep_rows, sweep_variant=args.sweep_variant)
     for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
         ctx.fill(fid, 0.0)
     ctx.set_density(1.0)
@@ -150,7 +152,8 @@ def main():
     cg_iter_ms = avg_a + avg_b
     cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_loc / (cg_iter_ms * 1e-3) / 1e9
 
-    traffic, traffic_src = pmc_traffic("k_cgA<", n_loc) if world == 1 else (None, None)
+    kname = f"k_cgA<{args.sweep_rows}, false, false, {args.sweep_variant}>"
+    traffic, traffic_src = pmc_traffic(kname, n_loc) if world == 1 else (None, None)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -202,9 +205,9 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(prefix, cells):
-    """HBM bytes per launch of the kernel from the committed PMC summary, if it
-    was recorded for this grid size (else None)."""
+def pmc_traffic(kname, cells):
+    """HBM bytes per launch of kernel `kname` from the committed PMC summary,
+    if it was recorded for this kernel variant and grid size (else None)."""
     try:
         d = json.loads(TRAFFIC_JSON.read_text())
     except (OSError, ValueError):
@@ -212,7 +215,7 @@ def pmc_traffic(prefix, cells):
     if d.get("cells_per_launch") != float(cells):
         return None, None
     for k, v in d.get("kernels", {}).items():
-        if k.startswith(prefix) and "true" not in k and "hbm_bytes_per_launch" in v:
+        if k == kname and "hbm_bytes_per_launch" in v:
             return round(v["hbm_bytes_per_launch"]), f"{TRAFFIC_JSON.name}: {k}"
     return None, None
 

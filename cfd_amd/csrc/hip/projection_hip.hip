@@ -41,28 +41,39 @@ static void launch_cgB_f(hip_proj_ctx* c, const Lap& L, const double* p, double*
     dist(c) ? launch_cgB_t<TY, true, FL>(c, L, p, r, it) : launch_cgB_t<TY, false, FL>(c, L, p, r, it);
 }
 
-// sweep_ty 4, 8 or 16; sweep_variant selects the SW_NT_* flags (TY 8 only)
+template <int TY>
+static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
+                         const double* po, double* pn, double* x, int it) {
+    switch (c->sweep_variant) {
+        case 1: return launch_cgA_f<TY, 1>(c, first, L, r, po, pn, x, it);
+        case 2: return launch_cgA_f<TY, 2>(c, first, L, r, po, pn, x, it);
+        case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, x, it);
+        default: return launch_cgA_f<TY, 0>(c, first, L, r, po, pn, x, it);
+    }
+}
+
+template <int TY>
+static void launch_cgB_v(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
+    switch (c->sweep_variant) {
+        case 1: return launch_cgB_f<TY, 1>(c, L, p, r, it);
+        case 2: return launch_cgB_f<TY, 2>(c, L, p, r, it);
+        case 3: return launch_cgB_f<TY, 3>(c, L, p, r, it);
+        default: return launch_cgB_f<TY, 0>(c, L, p, r, it);
+    }
+}
+
+// sweep_ty 8 or 16 (any sweep_variant), 4 (variant 0 only)
 static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
                        const double* po, double* pn, double* x, int it) {
     if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, x, it);
-    if (c->sweep_ty == 16) return launch_cgA_f<16, 0>(c, first, L, r, po, pn, x, it);
-    switch (c->sweep_variant) {
-        case 1: return launch_cgA_f<8, 1>(c, first, L, r, po, pn, x, it);
-        case 2: return launch_cgA_f<8, 2>(c, first, L, r, po, pn, x, it);
-        case 3: return launch_cgA_f<8, 3>(c, first, L, r, po, pn, x, it);
-        default: return launch_cgA_f<8, 0>(c, first, L, r, po, pn, x, it);
-    }
+    if (c->sweep_ty == 16) return launch_cgA_v<16>(c, first, L, r, po, pn, x, it);
+    return launch_cgA_v<8>(c, first, L, r, po, pn, x, it);
 }
 
 static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
     if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, L, p, r, it);
-    if (c->sweep_ty == 16) return launch_cgB_f<16, 0>(c, L, p, r, it);
-    switch (c->sweep_variant) {
-        case 1: return launch_cgB_f<8, 1>(c, L, p, r, it);
-        case 2: return launch_cgB_f<8, 2>(c, L, p, r, it);
-        case 3: return launch_cgB_f<8, 3>(c, L, p, r, it);
-        default: return launch_cgB_f<8, 0>(c, L, p, r, it);
-    }
+    if (c->sweep_ty == 16) return launch_cgB_v<16>(c, L, p, r, it);
+    return launch_cgB_v<8>(c, L, p, r, it);
 }
 
 // ---------------------------------------------------------------------------
@@ -360,7 +371,8 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.poll_interval = 64;
     c.kchunk = 0;
     c.verbose = 0;
-    c.sweep_rows = 8;
+    c.sweep_rows = 16;   // tools/sweep_bench.py at 512^3: 16 rows + NT hints fastest
+    c.sweep_variant = SW_NT_STORE | SW_NT_LOAD;
     return c;
 }
 
@@ -450,10 +462,11 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     if (c->cfg.kchunk > 0) {
         sg.kc = c->cfg.kchunk;
     } else {
-        // 64-plane z runs, shortened (down to 16) until there are >= 4
-        // workgroups per CU: a thin slab must still fill all 256 CUs
+        // 64-plane z runs, shortened (down to 16) until the launch has
+        // enough wavefronts for full occupancy (32 per CU): a thin slab must
+        // still fill all 256 CUs
         sg.kc = 64;
-        const long long want = 4LL * c->grid_cap / 8;
+        const long long want = 32LL * (c->grid_cap / 8) / c->sweep_ty;
         while (sg.kc > 16 &&
                (long long)sg.tiles_x * sg.tiles_y * ((nint_k + sg.kc - 1) / sg.kc) < want)
             sg.kc /= 2;

@@ -58,9 +58,10 @@ typedef struct {
     int poll_interval;            /* iterations launched between host convergence polls */
     int kchunk;                   /* z planes per CG sweep tile; 0 = auto (64) */
     int verbose;
-    int sweep_rows;               /* y rows (wavefronts) per CG sweep workgroup: 4, 8 or 16 */
+    int sweep_rows;               /* y rows (wavefronts) per CG sweep workgroup: 4, 8 or 16
+                                     (default 16) */
     int sweep_variant;            /* CG sweep memory hints: bit0 non-temporal stores,
-                                     bit1 non-temporal loads of single-use inputs */
+                                     bit1 non-temporal loads of single-use inputs (default 3) */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
