@@ -72,6 +72,12 @@ def dist_env():
 def main():
     args = parse()
     rank, world, local = dist_env()
+    if os.environ.get("CFD_BENCH_SHARED_GPU") == "1":
+        # rehearsal of the N-rank path on a 1-GPU box: every rank on device 0,
+        # each rank its own NCCL_HOSTID so RCCL accepts the shared device
+        # (its socket transport then stands in for xGMI; timings meaningless)
+        os.environ["NCCL_HOSTID"] = f"cfd-bench-rank{rank}"
+        local = 0
     import torch  # noqa: F401  (imported first: one HIP runtime in the process)
     import torch.distributed as dist
 
@@ -177,7 +183,7 @@ def main():
     traffic, traffic_src = pmc_traffic(kname, n_loc) if world == 1 else (None, None)
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline and not tg:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
         cpu = cpu_baseline(n, args, k_mean)
 
     if rank == 0:
