@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=512, help="points per axis")
+    ap.add_argument("--size", type=int, default=512, help="grid points per axis")
     ap.add_argument("--case", choices=("cavity", "tg"), default="cavity",
                     help="cavity: configs[2] (default, every N); tg: configs[3] Taylor-Green")
     ap.add_argument("--re", type=float, default=1000.0)
@@ -91,7 +91,7 @@ def main():
         raise SystemExit("bench: no HIP device")
     torch.cuda.set_device(local)
 
-    n = args.n
+    n = args.size
     tg = args.case == "tg"
     if tg:
         # configs[3]: Taylor-Green on [0, 2pi]^3, nu = 0.01, dt = 1e-3, periodic

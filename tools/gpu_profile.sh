@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-p1}
 N=${N:-512}
-ARGS=${ARGS:-"--n $N --steps 1 --warmup 1 --no-cpu-baseline"}
+ARGS=${ARGS:-"--size $N --steps 1 --warmup 1 --no-cpu-baseline"}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
