@@ -1,0 +1,67 @@
+"""bench.py's contract on the GPU: the JSON line the driver parses, at a small
+size, for one rank and for the N-rank Z-slab path (rehearsed on one GPU with
+CFD_BENCH_SHARED_GPU: every rank on device 0, RCCL over its socket
+transport). The 8-GPU run itself is the driver's."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parent.parent
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _last_json(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
+    return json.loads(lines[0])
+
+
+def _env():
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def test_bench_one_gpu_contract(hip_lib):
+    r = subprocess.run([sys.executable, "bench.py", "--size", "66", "--steps", "2", "--warmup",
+                        "1", "--cpu-cg-iters", "2"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0
+    assert d["unit"] == "MLUPS" and d["higher_is_better"] is True
+    assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
+    assert 0 < d["roofline"]["frac"] < 1
+    cpu = d["cpu_baseline"]
+    assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
+
+
+@pytest.mark.parametrize("case", ["cavity", "tg"])
+def test_bench_two_rank_rehearsal(hip_lib, case):
+    env = _env()
+    env["CFD_BENCH_SHARED_GPU"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "2",
+           "--size", "66", "--steps", "2", "--warmup", "1", "--case", case]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "strong"
+    assert d["cpu_baseline"] is None  # CPU baseline at N=1 only
+    assert "z-slab x2" in d["config"]["parallelism"]
