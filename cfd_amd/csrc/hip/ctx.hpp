@@ -59,6 +59,8 @@ struct hip_proj_ctx {
     long long px = 0, ps = 0;
     Geo geo{};
     SGeo sgeo{};       // row-pair CG sweep tiling
+    SGeo sg_edge{}, sg_int{};  // slabs: sweep B split into edge planes + interior
+    int split_b = 0;
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
     int sweep_variant = 0;  // SW_NT_* flags of the CG sweeps
     int grid_cap = 2048;

@@ -141,18 +141,20 @@ __device__ __forceinline__ bool grid_sum_last(double block_total, double* partia
 template <int NTH>
 __device__ __forceinline__ bool grid_sum_last_n(double block_total, double* partials,
                                                 unsigned* counter, double* sh, int* flag,
-                                                double& total) {
+                                                double& total, unsigned pofs = 0,
+                                                unsigned ptot = 0) {
+    if (ptot == 0) ptot = gridDim.x;
     if (threadIdx.x == 0) {
-        store_sc1(&partials[blockIdx.x], block_total);
+        store_sc1(&partials[pofs + blockIdx.x], block_total);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
-        *flag = (t == gridDim.x - 1) ? 1 : 0;
+        *flag = (t == ptot - 1) ? 1 : 0;
     }
     __syncthreads();
     if (*flag == 0) return false;
     double s = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += NTH) s += load_sc1(&partials[b]);
+    for (unsigned b = threadIdx.x; b < ptot; b += NTH) s += load_sc1(&partials[b]);
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
     __syncthreads();
@@ -365,6 +367,14 @@ struct SGeo {
     long long px, ps, sz;
     int k0, k1, kc;
     int tiles_x, tiles_y, tiles_z;  // tiles of 128 x TY x kc
+    // kmode 1: the two slab-edge planes only (tz 0 -> plane k0, tz 1 -> k1-1),
+    // one plane per tile; the launch covering the remaining planes uses
+    // k0+1 .. k1-1. A sweep split over several launches shares one partials
+    // array: this launch's workgroups own partials [part_ofs, part_ofs +
+    // gridDim.x) of part_total, and the last of all part_total workgroups
+    // (same stream, so the later launch) finishes the reduction.
+    int kmode;
+    int part_ofs, part_total;
 };
 
 __device__ __forceinline__ int xcd_tile(int b, int nt) {
@@ -425,8 +435,13 @@ __device__ __forceinline__ RowPair row_pair(const SGeo& g) {
     c.w = threadIdx.x >> 6;
     c.i0 = tx * 128 + 2 * c.lane;
     c.j = ty * TY + c.w;
-    c.kb = g.k0 + tz * g.kc;
-    c.ke = min(c.kb + g.kc, g.k1);
+    if (g.kmode == 1) {
+        c.kb = (tz == 0) ? g.k0 : g.k1 - 1;
+        c.ke = c.kb + 1;
+    } else {
+        c.kb = g.k0 + tz * g.kc;
+        c.ke = min(c.kb + g.kc, g.k1);
+    }
     c.act = (c.j >= 1) && (c.j <= g.ny - 2) && (c.i0 < g.nx);
     c.in0 = c.act && (c.i0 >= 1) && (c.i0 <= g.nx - 2);
     c.in1 = c.act && (c.i0 + 1 <= g.nx - 2);
@@ -602,7 +617,7 @@ static __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const dou
         for (int q = 0; q < TY; ++q) bt += sh[q];
     double tot;
     double* shs = (double*)&rows[0][0][0];
-    if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
+    if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot, g.part_ofs, g.part_total) && threadIdx.x == 0) {
         if (DIST) dsum[0] = tot;
         else fin_B(st, tot, it);
     }

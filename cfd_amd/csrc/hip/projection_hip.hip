@@ -20,10 +20,11 @@ static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const d
 }
 
 template <int TY, bool DIST, int FL>
-static void launch_cgB_t(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
-                          c->stream, c->ta, c->tb, 0, c->sgeo, L, p, r, c->st, c->partials,
-                          c->counter, it, c->dsum);
+static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p,
+                         double* r, int it) {
+    const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
+    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(nb), dim3(64 * TY), 0, c->stream, c->ta,
+                          c->tb, 0, sg, L, p, r, c->st, c->partials, c->counter, it, c->dsum);
 }
 
 template <int TY, int FL>
@@ -37,8 +38,10 @@ static void launch_cgA_f(hip_proj_ctx* c, bool first, const Lap& L, const double
 }
 
 template <int TY, int FL>
-static void launch_cgB_f(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    dist(c) ? launch_cgB_t<TY, true, FL>(c, L, p, r, it) : launch_cgB_t<TY, false, FL>(c, L, p, r, it);
+static void launch_cgB_f(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p,
+                         double* r, int it) {
+    dist(c) ? launch_cgB_t<TY, true, FL>(c, sg, L, p, r, it)
+            : launch_cgB_t<TY, false, FL>(c, sg, L, p, r, it);
 }
 
 template <int TY>
@@ -53,12 +56,13 @@ static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double
 }
 
 template <int TY>
-static void launch_cgB_v(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
+static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p,
+                         double* r, int it) {
     switch (c->sweep_variant) {
-        case 1: return launch_cgB_f<TY, 1>(c, L, p, r, it);
-        case 2: return launch_cgB_f<TY, 2>(c, L, p, r, it);
-        case 3: return launch_cgB_f<TY, 3>(c, L, p, r, it);
-        default: return launch_cgB_f<TY, 0>(c, L, p, r, it);
+        case 1: return launch_cgB_f<TY, 1>(c, sg, L, p, r, it);
+        case 2: return launch_cgB_f<TY, 2>(c, sg, L, p, r, it);
+        case 3: return launch_cgB_f<TY, 3>(c, sg, L, p, r, it);
+        default: return launch_cgB_f<TY, 0>(c, sg, L, p, r, it);
     }
 }
 
@@ -70,10 +74,11 @@ static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* 
     return launch_cgA_v<8>(c, first, L, r, po, pn, x, it);
 }
 
-static void launch_cgB(hip_proj_ctx* c, const Lap& L, const double* p, double* r, int it) {
-    if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, L, p, r, it);
-    if (c->sweep_ty == 16) return launch_cgB_v<16>(c, L, p, r, it);
-    return launch_cgB_v<8>(c, L, p, r, it);
+static void launch_cgB(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p, double* r,
+                       int it) {
+    if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, sg, L, p, r, it);
+    if (c->sweep_ty == 16) return launch_cgB_v<16>(c, sg, L, p, r, it);
+    return launch_cgB_v<8>(c, sg, L, p, r, it);
 }
 
 // ---------------------------------------------------------------------------
@@ -136,15 +141,22 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
             ST_TRY(reduce_dot(c));
             hipExtLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
         }
-        timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, L, pnew, c->r, it); }, it);
+        if (!D) timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sgeo, L, pnew, c->r, it); }, it);
         if (D) {
-            // r's halo goes out on the side stream (halo communicator) while
-            // the main stream all-reduces (r,r); the next sweep A waits for both
+            // r's halo goes out on the side stream (halo communicator) as soon
+            // as the two slab-edge planes of the new r exist: sweep B runs them
+            // first, then the interior planes overlap the exchange; the (r,r)
+            // all-reduce follows on the main stream; the next sweep A waits
+            // for both
+            if (c->split_b) launch_cgB(c, c->sg_edge, L, pnew, c->r, it);
+            else timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sgeo, L, pnew, c->r, it); }, it);
             HIP_TRY(hipEventRecord(c->ev_b, c->stream));
             HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
             double* rr[1] = {c->r};
             ST_TRY(c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false));
             HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
+            if (c->split_b)
+                timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sg_int, L, pnew, c->r, it); }, it);
             ST_TRY(reduce_dot(c));
             hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
@@ -473,7 +485,29 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     }
     sg.kc = std::max(1, std::min(sg.kc, nint_k));
     sg.tiles_z = (nint_k + sg.kc - 1) / sg.kc;
-    const int n_partials = std::max(c->grid_cap, sg.tiles_x * sg.tiles_y * sg.tiles_z);
+    int n_partials = std::max(c->grid_cap, sg.tiles_x * sg.tiles_y * sg.tiles_z);
+    c->split_b = (c->nranks > 1 && nint_k >= 3) ? 1 : 0;
+    if (c->split_b) {
+        // sweep B on slabs: the two edge planes (what the neighbours need)
+        // first, then planes k0+1 .. k1-1; one reduction over both launches
+        SGeo& e = c->sg_edge;
+        SGeo& m = c->sg_int;
+        e = sg;
+        e.kmode = 1;
+        e.kc = 1;
+        e.tiles_z = 2;
+        m = sg;
+        m.k0 = sg.k0 + 1;
+        m.k1 = sg.k1 - 1;
+        m.kc = std::max(1, std::min(sg.kc, m.k1 - m.k0));
+        m.tiles_z = (m.k1 - m.k0 + m.kc - 1) / m.kc;
+        const int ne = e.tiles_x * e.tiles_y * e.tiles_z;
+        const int nm = m.tiles_x * m.tiles_y * m.tiles_z;
+        e.part_ofs = 0;
+        m.part_ofs = ne;
+        e.part_total = m.part_total = ne + nm;
+        n_partials = std::max(n_partials, ne + nm);
+    }
 
     const size_t n = field_elems(c);
     double** fields[] = {&c->u, &c->v, &c->w, &c->p, &c->us, &c->vs, &c->ws, &c->pn,
