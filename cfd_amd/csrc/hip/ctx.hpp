@@ -200,6 +200,11 @@ static int sweep_grid(const hip_proj_ctx* c) {
 
 static bool dist(const hip_proj_ctx* c) { return c->nranks > 1; }
 
+// one-shot device all-reduce mailbox of the slab communicator (or nullptr)
+static inline Mbox* mbox(const hip_proj_ctx* c) {
+    return (c->nranks > 1 && c->comm) ? c->comm->device_mailbox() : nullptr;
+}
+
 static dim3 cell_grid(const hip_proj_ctx* c) {
     return dim3((unsigned)((c->nx + 63) / 64), (unsigned)((c->ny + 3) / 4), (unsigned)c->nz);
 }

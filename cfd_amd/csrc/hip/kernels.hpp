@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mbox.hpp"
+
 namespace cfdhip {
 
 constexpr int TX = 64;       // x extent of a tile = one wavefront
@@ -272,6 +274,51 @@ __device__ __forceinline__ void fin_B(CgState* st, double tot, int it) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// One-shot device all-reduce over peer memory (Z-slabs, opt-in): the last
+// workgroup of a sweep writes its total into slot [parity][rank] of every
+// rank's mailbox (system-scope stores over xGMI), then waits until all ranks'
+// slots carry the same sequence number and sums them in rank order, so every
+// rank holds the same bits. The sequence counter lives on the device and
+// advances only when a reduction actually runs, so consecutive reductions
+// alternate parity and a slot is never overwritten before its reader has
+// consumed it. A bounded wait (timeout_ticks of wall_clock64) turns a lost
+// peer into a reported error instead of a hung GPU.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool mbox_allreduce(Mbox* mb, double v, double* out) {
+    const unsigned long long seq = mb->count + 1;
+    mb->count = seq;
+    const int n = mb->n, me = mb->rank;
+    const int par = (int)(seq & 1ull);
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+    for (int r = 0; r < n; ++r) {
+        unsigned long long* s = mb->slot[r] + 2 * (par * MBOX_MAX + me);
+        __hip_atomic_store(s, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(s + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    unsigned long long* mine = mb->slot[me];
+    const long long t0 = wall_clock64();
+    double sum = 0.0;
+    for (int r = 0; r < n; ++r) {
+        unsigned long long* s = mine + 2 * (par * MBOX_MAX + r);
+        while (__hip_atomic_load(s + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > mb->timeout_ticks) return false;
+        }
+        sum += __longlong_as_double(
+            (long long)__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    *out = sum;
+    return true;
+}
+
+constexpr int ST_COMM_TIMEOUT = 9;
+
+__device__ __forceinline__ void comm_fail(CgState* st) {
+    st->done = 1;
+    st->status = ST_COMM_TIMEOUT;
+}
+
 static __global__ void k_finish_setup(CgState* st, const double* tot, double rel_tol, double abs_tol,
                                int max_iter, int check_interval) {
     if (threadIdx.x == 0) fin_setup(st, tot[0], rel_tol, abs_tol, max_iter, check_interval);
@@ -306,7 +353,8 @@ static __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc
                                                  double* __restrict__ r, CgState* st,
                                                  double* partials, unsigned* counter,
                                                  double rel_tol, double abs_tol, int max_iter,
-                                                 int check_interval, double* dsum) {
+                                                 int check_interval, double* dsum,
+                                                 Mbox* mb) {
     __shared__ double sh[NWAVE];
     __shared__ int flag;
     double acc = 0.0;
@@ -343,8 +391,15 @@ static __global__ __launch_bounds__(NT) void k_cg_setup(Geo g, Lap L, DivCoef dc
     double bt = block_sum(acc, sh);
     double tot;
     if (grid_sum_last(bt, partials, counter, sh, &flag, tot) && threadIdx.x == 0) {
-        if (DIST) dsum[0] = tot;
-        else fin_setup(st, tot, rel_tol, abs_tol, max_iter, check_interval);
+        if (DIST && mb) {
+            double g;
+            if (mbox_allreduce(mb, tot, &g)) fin_setup(st, g, rel_tol, abs_tol, max_iter, check_interval);
+            else comm_fail(st);
+        } else if (DIST) {
+            dsum[0] = tot;
+        } else {
+            fin_setup(st, tot, rel_tol, abs_tol, max_iter, check_interval);
+        }
     }
 }
 
@@ -458,7 +513,7 @@ static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const dou
                                                  const double* __restrict__ po,
                                                  double* __restrict__ pn, double* __restrict__ x,
                                                  CgState* st, double* partials, unsigned* counter,
-                                                 int it, double* dsum) {
+                                                 int it, double* dsum, Mbox* mb) {
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
@@ -550,8 +605,15 @@ static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const dou
     double tot;
     double* shs = (double*)&rows[0][0][0];
     if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
-        if (DIST) dsum[0] = tot;
-        else fin_A(st, tot, it);
+        if (DIST && mb) {
+            double g;
+            if (mbox_allreduce(mb, tot, &g)) fin_A(st, g, it);
+            else comm_fail(st);
+        } else if (DIST) {
+            dsum[0] = tot;
+        } else {
+            fin_A(st, tot, it);
+        }
     }
 }
 
@@ -561,7 +623,7 @@ template <int TY, bool DIST, int FL = 0>
 static __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
                                                  double* __restrict__ r, CgState* st,
                                                  double* partials, unsigned* counter, int it,
-                                                 double* dsum) {
+                                                 double* dsum, Mbox* mb) {
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
@@ -617,9 +679,18 @@ static __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const dou
         for (int q = 0; q < TY; ++q) bt += sh[q];
     double tot;
     double* shs = (double*)&rows[0][0][0];
-    if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot, g.part_ofs, g.part_total) && threadIdx.x == 0) {
-        if (DIST) dsum[0] = tot;
-        else fin_B(st, tot, it);
+    if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot, g.part_ofs,
+                                 g.part_total) &&
+        threadIdx.x == 0) {
+        if (DIST && mb) {
+            double g2;
+            if (mbox_allreduce(mb, tot, &g2)) fin_B(st, g2, it);
+            else comm_fail(st);
+        } else if (DIST) {
+            dsum[0] = tot;
+        } else {
+            fin_B(st, tot, it);
+        }
     }
 }
 

@@ -16,7 +16,7 @@ static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const d
                          double* pn, double* x, int it) {
     hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST, FL>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
                           c->stream, c->ta, c->tb, 0, c->sgeo, L, r, po, pn, x, c->st,
-                          c->partials, c->counter, it, c->dsum);
+                          c->partials, c->counter, it, c->dsum, mbox(c));
 }
 
 template <int TY, bool DIST, int FL>
@@ -24,7 +24,8 @@ static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const do
                          double* r, int it) {
     const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
     hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(nb), dim3(64 * TY), 0, c->stream, c->ta,
-                          c->tb, 0, sg, L, p, r, c->st, c->partials, c->counter, it, c->dsum);
+                          c->tb, 0, sg, L, p, r, c->st, c->partials, c->counter, it, c->dsum,
+                          mbox(c));
 }
 
 template <int TY, int FL>
@@ -104,31 +105,31 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                 hipExtLaunchKernelGGL((k_cg_setup<true, false, true, true>), dim3(G), dim3(NT), 0,
                                    c->stream, c->ta, c->tb, 0, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
                                    c->r, c->st, c->partials, c->counter, rel_tol, abs_tol,
-                                   max_iter, check_interval, c->dsum);
+                                   max_iter, check_interval, c->dsum, mbox(c));
             else
                 hipExtLaunchKernelGGL((k_cg_setup<true, false, true, false>), dim3(G), dim3(NT), 0,
                                    c->stream, c->ta, c->tb, 0, c->geo, L, dc, c->us, c->vs, c->ws, nullptr, x,
                                    c->r, c->st, c->partials, c->counter, rel_tol, abs_tol,
-                                   max_iter, check_interval, c->dsum);
+                                   max_iter, check_interval, c->dsum, (Mbox*)nullptr);
         } else {
             if (D)
                 hipExtLaunchKernelGGL((k_cg_setup<false, false, true, true>), dim3(G), dim3(NT), 0,
                                    c->stream, c->ta, c->tb, 0, c->geo, L, dc, nullptr, nullptr, nullptr,
                                    (double*)rhs_in, x, c->r, c->st, c->partials, c->counter,
-                                   rel_tol, abs_tol, max_iter, check_interval, c->dsum);
+                                   rel_tol, abs_tol, max_iter, check_interval, c->dsum, mbox(c));
             else
                 hipExtLaunchKernelGGL((k_cg_setup<false, false, true, false>), dim3(G), dim3(NT), 0,
                                    c->stream, c->ta, c->tb, 0, c->geo, L, dc, nullptr, nullptr, nullptr,
                                    (double*)rhs_in, x, c->r, c->st, c->partials, c->counter,
-                                   rel_tol, abs_tol, max_iter, check_interval, c->dsum);
+                                   rel_tol, abs_tol, max_iter, check_interval, c->dsum, (Mbox*)nullptr);
         }
     });
-    if (D) {
+    if (D && !mbox(c)) {
         ST_TRY(reduce_dot(c));
-        hipExtLaunchKernelGGL(k_finish_setup, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1,
-                           rel_tol, abs_tol, max_iter, check_interval);
-        ST_TRY(halo(c, {c->r}));
+        hipExtLaunchKernelGGL(k_finish_setup, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
+                              c->st, c->dsum + 1, rel_tol, abs_tol, max_iter, check_interval);
     }
+    if (D) ST_TRY(halo(c, {c->r}));
     double* P[2] = {c->pa, c->pb};
     // one CG iteration: sweep A (+ all-reduce of (p,Ap); on slabs A also
     // forms p on the halo planes), sweep B (+ all-reduce of (r,r), halo of r)
@@ -137,7 +138,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         double* pold = P[(it + 1) & 1];
         timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, x, it); },
               it);
-        if (D) {
+        if (D && !mbox(c)) {
             ST_TRY(reduce_dot(c));
             hipExtLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
         }
@@ -157,8 +158,11 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
             HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
             if (c->split_b)
                 timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sg_int, L, pnew, c->r, it); }, it);
-            ST_TRY(reduce_dot(c));
-            hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
+            if (!mbox(c)) {
+                ST_TRY(reduce_dot(c));
+                hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
+                                      c->st, c->dsum + 1, it);
+            }
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
         }
         return CFD_SUCCESS;
@@ -195,6 +199,10 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     HIP_TRY(hipStreamSynchronize(c->stream));
     const CgState& s = c->h_state[2];
     flush_timing(c, s.iterations);
+    if (s.status == ST_COMM_TIMEOUT) {
+        set_err(CFD_ERROR, "projection_hip: slab all-reduce timed out (a rank stopped)");
+        return CFD_ERROR;
+    }
     const bool stagnated = (s.status == ST_STAGNATED);
     // final poisson_solver_apply_bc (cg.c:447); the breakdown exit skips it.
     if (final_bc && !stagnated && !(s.iterations == 0 && s.status == ST_CONVERGED))
@@ -956,7 +964,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
         const int G = tile_grid(c);
         hipExtLaunchKernelGGL((k_cg_setup<true, true, false>), dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0,
                            c->geo, L, dc, c->us, c->vs, c->ws, c->rhs, c->pn, c->r, c->st,
-                           c->partials, c->counter, 0.0, 0.0, 0, 1, c->dsum);
+                           c->partials, c->counter, 0.0, 0.0, 0, 1, c->dsum, (Mbox*)nullptr);
         if (method == HIP_POISSON_JACOBI)
             HIP_TRY(hipMemsetAsync(c->xt, 0, field_elems(c) * sizeof(double), c->stream));
         int maxit = c->cfg.poisson_max_iter;

@@ -2,6 +2,8 @@
 // and their C-ABI constructors (include/cfd_hip/projection_hip.h).
 #include "slab_comm.hpp"
 
+#include "mbox.hpp"
+
 #include "cfd_hip/projection_hip.h"
 
 #include <rccl/rccl.h>
@@ -47,10 +49,20 @@ struct RcclComm final : SlabComm {
     ncclComm_t comm = nullptr;   // all-reduces
     ncclComm_t hcomm = nullptr;  // halo send/recv: its own communicator, so a
                                  // halo on a side stream may overlap an all-reduce
+    // opt-in device mailbox (CFD_HIP_DEVICE_ALLREDUCE=1)
+    void* mbox = nullptr;                    // own mailbox (uncached device memory)
+    std::vector<void*> peer_open;            // peers' mailboxes mapped through IPC
+    cfdhip::Mbox* d_mb = nullptr;            // device copy of the Mbox descriptor
     ~RcclComm() override {
+        for (void* p : peer_open)
+            if (p) hipIpcCloseMemHandle(p);
+        if (d_mb) hipFree(d_mb);
+        if (mbox) hipFree(mbox);
         if (hcomm) ncclCommDestroy(hcomm);
         if (comm) ncclCommDestroy(comm);
     }
+    cfdhip::Mbox* device_mailbox() override { return d_mb; }
+    cfd_status_t setup_mailbox();
     // Posting order matters only when both neighbours are the same peer
     // (2 ranks, periodic): sends go to-lower then to-upper, receives come
     // from-upper then from-lower, so the k-th send to a peer always pairs
@@ -79,6 +91,58 @@ struct RcclComm final : SlabComm {
         return CFD_SUCCESS;
     }
 };
+
+// Every rank allocates a small uncached mailbox, exports it through IPC, and
+// the handles are all-gathered over RCCL; each rank then maps every peer's
+// mailbox (xGMI peer access) into its Mbox descriptor.
+cfd_status_t RcclComm::setup_mailbox() {
+    constexpr size_t MB_BYTES = 4096;
+    static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+    HIPC(hipExtMallocWithFlags(&mbox, MB_BYTES, hipDeviceMallocUncached));
+    HIPC(hipMemset(mbox, 0, MB_BYTES));
+    hipIpcMemHandle_t h;
+    HIPC(hipIpcGetMemHandle(&h, mbox));
+    unsigned char *d_send = nullptr, *d_recv = nullptr;
+    HIPC(hipMalloc((void**)&d_send, 64));
+    HIPC(hipMalloc((void**)&d_recv, 64 * (size_t)size));
+    HIPC(hipMemset(d_send, 0, 64));
+    HIPC(hipMemcpy(d_send, &h, sizeof(h), hipMemcpyHostToDevice));
+    hipStream_t s;
+    HIPC(hipStreamCreate(&s));
+    ncclResult_t r = ncclAllGather(d_send, d_recv, 64, ncclUint8, comm, s);
+    hipError_t e = hipStreamSynchronize(s);
+    hipStreamDestroy(s);
+    std::vector<unsigned char> all(64 * (size_t)size);
+    hipError_t e2 = hipMemcpy(all.data(), d_recv, all.size(), hipMemcpyDeviceToHost);
+    hipFree(d_send);
+    hipFree(d_recv);
+    if (r != ncclSuccess) return fail(CFD_ERROR, "ncclAllGather (mailbox handles)", ncclGetErrorString(r));
+    HIPC(e);
+    HIPC(e2);
+    cfdhip::Mbox hmb{};
+    hmb.n = size;
+    hmb.rank = rank;
+    hmb.count = 0;
+    int rate_khz = 0;
+    HIPC(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device));
+    hmb.timeout_ticks = (long long)std::max(rate_khz, 1000) * 1000LL * 20;  // 20 s
+    peer_open.assign(size, nullptr);
+    for (int q = 0; q < size; ++q) {
+        if (q == rank) {
+            hmb.slot[q] = (unsigned long long*)mbox;
+            continue;
+        }
+        hipIpcMemHandle_t ph;
+        memcpy(&ph, all.data() + 64 * (size_t)q, sizeof(ph));
+        void* p = nullptr;
+        HIPC(hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess));
+        peer_open[q] = p;
+        hmb.slot[q] = (unsigned long long*)p;
+    }
+    HIPC(hipMalloc((void**)&d_mb, sizeof(hmb)));
+    HIPC(hipMemcpy(d_mb, &hmb, sizeof(hmb), hipMemcpyHostToDevice));
+    return CFD_SUCCESS;
+}
 
 // ---------------------------------------------------------------------------
 // In-process group: each rank's host thread publishes what it exposes,
@@ -263,6 +327,14 @@ hip_proj_comm_t* hip_proj_comm_create_rccl(const unsigned char id[HIP_PROJ_UNIQU
         c->hcomm = nullptr;
         delete c;
         return nullptr;
+    }
+    const char* mb = getenv("CFD_HIP_DEVICE_ALLREDUCE");
+    if (size > 1 && size <= cfdhip::MBOX_MAX && mb && atoi(mb) == 1) {
+        // a failure here is collective-safe: every rank ran the same all-gather
+        if (c->setup_mailbox() != CFD_SUCCESS) {
+            delete c;
+            return nullptr;
+        }
     }
     auto* h = new hip_proj_comm();
     h->impl = c;

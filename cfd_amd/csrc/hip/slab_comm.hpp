@@ -17,6 +17,10 @@
 
 #include "cfd_hip/cfd_abi.h"
 
+namespace cfdhip {
+struct Mbox;
+}
+
 struct SlabComm {
     int rank = 0, size = 1, device = 0;
     virtual ~SlabComm() {}
@@ -30,6 +34,9 @@ struct SlabComm {
     virtual cfd_status_t allreduce_sum(hipStream_t s, const double* in, double* out, int n) = 0;
     virtual cfd_status_t allreduce_max_u64(hipStream_t s, const unsigned long long* in,
                                            unsigned long long* out, int n) = 0;
+    // Device mailbox for the one-shot CG dot all-reduce fused into the sweeps
+    // (kernels.hpp mbox_allreduce); nullptr = all-reduce through allreduce_sum.
+    virtual cfdhip::Mbox* device_mailbox() { return nullptr; }
 };
 
 struct hip_proj_comm {

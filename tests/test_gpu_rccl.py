@@ -18,8 +18,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_rccl_two_rank_slabs(hip_lib):
+@pytest.mark.parametrize("device_allreduce", ["0", "1"])
+def test_rccl_two_rank_slabs(hip_lib, device_allreduce):
+    """device_allreduce=1: CG dots through the one-shot peer-memory mailbox
+    (IPC-mapped between the two processes) instead of ncclAllReduce."""
     env = dict(os.environ)
+    env["CFD_HIP_DEVICE_ALLREDUCE"] = device_allreduce
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
