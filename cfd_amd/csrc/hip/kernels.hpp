@@ -274,44 +274,6 @@ __device__ __forceinline__ void fin_B(CgState* st, double tot, int it) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// One-shot device all-reduce over peer memory (Z-slabs, opt-in): the last
-// workgroup of a sweep writes its total into slot [parity][rank] of every
-// rank's mailbox (system-scope stores over xGMI), then waits until all ranks'
-// slots carry the same sequence number and sums them in rank order, so every
-// rank holds the same bits. The sequence counter lives on the device and
-// advances only when a reduction actually runs, so consecutive reductions
-// alternate parity and a slot is never overwritten before its reader has
-// consumed it. A bounded wait (timeout_ticks of wall_clock64) turns a lost
-// peer into a reported error instead of a hung GPU.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool mbox_allreduce(Mbox* mb, double v, double* out) {
-    const unsigned long long seq = mb->count + 1;
-    mb->count = seq;
-    const int n = mb->n, me = mb->rank;
-    const int par = (int)(seq & 1ull);
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
-    for (int r = 0; r < n; ++r) {
-        unsigned long long* s = mb->slot[r] + 2 * (par * MBOX_MAX + me);
-        __hip_atomic_store(s, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(s + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    unsigned long long* mine = mb->slot[me];
-    const long long t0 = wall_clock64();
-    double sum = 0.0;
-    for (int r = 0; r < n; ++r) {
-        unsigned long long* s = mine + 2 * (par * MBOX_MAX + r);
-        while (__hip_atomic_load(s + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > mb->timeout_ticks) return false;
-        }
-        sum += __longlong_as_double(
-            (long long)__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    }
-    *out = sum;
-    return true;
-}
-
 constexpr int ST_COMM_TIMEOUT = 9;
 
 __device__ __forceinline__ void comm_fail(CgState* st) {

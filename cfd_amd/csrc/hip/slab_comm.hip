@@ -98,27 +98,33 @@ struct RcclComm final : SlabComm {
 cfd_status_t RcclComm::setup_mailbox() {
     constexpr size_t MB_BYTES = 4096;
     static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
-    HIPC(hipExtMallocWithFlags(&mbox, MB_BYTES, hipDeviceMallocUncached));
-    HIPC(hipMemset(mbox, 0, MB_BYTES));
-    hipIpcMemHandle_t h;
-    HIPC(hipIpcGetMemHandle(&h, mbox));
+    // local part; whatever happens here, every rank still joins the all-gather
+    unsigned char hbytes[64] = {0};
+    bool local = hipExtMallocWithFlags(&mbox, MB_BYTES, hipDeviceMallocUncached) == hipSuccess &&
+                 hipMemset(mbox, 0, MB_BYTES) == hipSuccess;
+    if (local) {
+        hipIpcMemHandle_t h;
+        local = hipIpcGetMemHandle(&h, mbox) == hipSuccess;
+        if (local) memcpy(hbytes, &h, sizeof(h));
+    }
+    (void)hipGetLastError();
     unsigned char *d_send = nullptr, *d_recv = nullptr;
+    hipStream_t s = nullptr;
+    std::vector<unsigned char> all(64 * (size_t)size, 0);
     HIPC(hipMalloc((void**)&d_send, 64));
     HIPC(hipMalloc((void**)&d_recv, 64 * (size_t)size));
-    HIPC(hipMemset(d_send, 0, 64));
-    HIPC(hipMemcpy(d_send, &h, sizeof(h), hipMemcpyHostToDevice));
-    hipStream_t s;
+    HIPC(hipMemcpy(d_send, hbytes, 64, hipMemcpyHostToDevice));
     HIPC(hipStreamCreate(&s));
     ncclResult_t r = ncclAllGather(d_send, d_recv, 64, ncclUint8, comm, s);
     hipError_t e = hipStreamSynchronize(s);
     hipStreamDestroy(s);
-    std::vector<unsigned char> all(64 * (size_t)size);
     hipError_t e2 = hipMemcpy(all.data(), d_recv, all.size(), hipMemcpyDeviceToHost);
     hipFree(d_send);
     hipFree(d_recv);
     if (r != ncclSuccess) return fail(CFD_ERROR, "ncclAllGather (mailbox handles)", ncclGetErrorString(r));
     HIPC(e);
     HIPC(e2);
+    if (!local) return fail(CFD_ERROR, "mailbox allocation / IPC export failed", nullptr);
     cfdhip::Mbox hmb{};
     hmb.n = size;
     hmb.rank = rank;
@@ -142,6 +148,60 @@ cfd_status_t RcclComm::setup_mailbox() {
     HIPC(hipMalloc((void**)&d_mb, sizeof(hmb)));
     HIPC(hipMemcpy(d_mb, &hmb, sizeof(hmb), hipMemcpyHostToDevice));
     return CFD_SUCCESS;
+}
+
+namespace {
+__global__ void k_mbox_selftest(cfdhip::Mbox* mb, double v, double* out, int* ok) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double s = 0.0;
+        *ok = cfdhip::mbox_allreduce(mb, v, &s) ? 1 : 0;
+        *out = s;
+    }
+}
+}  // namespace
+
+// Collective: every rank reports whether its mailbox is set up and a one-shot
+// all-reduce of rank+1 over it returns n(n+1)/2 within ~2 s; the mailbox stays
+// enabled only if that holds on every rank (else all fall back to RCCL).
+static bool mailbox_verified(RcclComm* c, bool local_ok) {
+    int ok = 0;
+    if (local_ok) {
+        cfdhip::Mbox h{};
+        hipMemcpy(&h, c->d_mb, sizeof(h), hipMemcpyDeviceToHost);
+        const long long full = h.timeout_ticks;
+        h.timeout_ticks = full / 10;  // short bound for the probe
+        hipMemcpy(c->d_mb, &h, sizeof(h), hipMemcpyHostToDevice);
+        double* d_out = nullptr;
+        int* d_ok = nullptr;
+        if (hipMalloc((void**)&d_out, sizeof(double)) == hipSuccess &&
+            hipMalloc((void**)&d_ok, sizeof(int)) == hipSuccess) {
+            hipLaunchKernelGGL(k_mbox_selftest, dim3(1), dim3(64), 0, 0, c->d_mb,
+                               (double)(c->rank + 1), d_out, d_ok);
+            double out = 0.0;
+            int kok = 0;
+            if (hipDeviceSynchronize() == hipSuccess &&
+                hipMemcpy(&out, d_out, sizeof(double), hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(&kok, d_ok, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess)
+                ok = (kok == 1 && out == 0.5 * c->size * (c->size + 1)) ? 1 : 0;
+        }
+        if (d_out) hipFree(d_out);
+        if (d_ok) hipFree(d_ok);
+        hipMemcpy(&h, c->d_mb, sizeof(h), hipMemcpyDeviceToHost);  // keeps count
+        h.timeout_ticks = full;
+        hipMemcpy(c->d_mb, &h, sizeof(h), hipMemcpyHostToDevice);
+    }
+    int* d_flag = nullptr;
+    int all = 0;
+    hipStream_t s = nullptr;
+    if (hipMalloc((void**)&d_flag, sizeof(int)) == hipSuccess && hipStreamCreate(&s) == hipSuccess) {
+        hipMemcpy(d_flag, &ok, sizeof(int), hipMemcpyHostToDevice);
+        if (ncclAllReduce(d_flag, d_flag, 1, ncclInt32, ncclMin, c->comm, s) == ncclSuccess &&
+            hipStreamSynchronize(s) == hipSuccess)
+            hipMemcpy(&all, d_flag, sizeof(int), hipMemcpyDeviceToHost);
+    }
+    if (s) hipStreamDestroy(s);
+    if (d_flag) hipFree(d_flag);
+    return all == 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -328,12 +388,20 @@ hip_proj_comm_t* hip_proj_comm_create_rccl(const unsigned char id[HIP_PROJ_UNIQU
         delete c;
         return nullptr;
     }
+    // one-shot device all-reduce for the CG dots; default on, CFD_HIP_DEVICE_ALLREDUCE=0
+    // keeps every dot on ncclAllReduce
     const char* mb = getenv("CFD_HIP_DEVICE_ALLREDUCE");
-    if (size > 1 && size <= cfdhip::MBOX_MAX && mb && atoi(mb) == 1) {
-        // a failure here is collective-safe: every rank ran the same all-gather
-        if (c->setup_mailbox() != CFD_SUCCESS) {
-            delete c;
-            return nullptr;
+    if (size > 1 && size <= cfdhip::MBOX_MAX && !(mb && atoi(mb) == 0)) {
+        const bool local_ok = (c->setup_mailbox() == CFD_SUCCESS);
+        if (!mailbox_verified(c, local_ok)) {
+            for (void* p : c->peer_open)
+                if (p) hipIpcCloseMemHandle(p);
+            c->peer_open.clear();
+            if (c->d_mb) hipFree(c->d_mb);
+            c->d_mb = nullptr;
+            if (c->mbox) hipFree(c->mbox);
+            c->mbox = nullptr;
+            (void)hipGetLastError();
         }
     }
     auto* h = new hip_proj_comm();

@@ -20,8 +20,9 @@ def _free_port():
 
 @pytest.mark.parametrize("device_allreduce", ["0", "1"])
 def test_rccl_two_rank_slabs(hip_lib, device_allreduce):
-    """device_allreduce=1: CG dots through the one-shot peer-memory mailbox
-    (IPC-mapped between the two processes) instead of ncclAllReduce."""
+    """device_allreduce=1 (the default): CG dots through the one-shot
+    peer-memory mailbox (IPC-mapped between the two processes, verified by a
+    collective probe at communicator creation); 0: ncclAllReduce."""
     env = dict(os.environ)
     env["CFD_HIP_DEVICE_ALLREDUCE"] = device_allreduce
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
