@@ -205,8 +205,9 @@ def main():
                                     f"{n}^3 lid-driven cavity Re={args.re:g}, dt={args.dt:g}")
                                    + ", projection_hip (CG rel 1e-6)",
                        "grid": [n, n, n], "interior_cells": n_int,
-                       "parallelism": f"z-slab x{world} (RCCL halo + allreduce)" if world > 1
-                       else "single GPU"},
+                       "parallelism": (f"z-slab x{world} (RCCL halo, "
+                                       + ("peer-memory" if comm.device_allreduce else "RCCL")
+                                       + " dot all-reduce)") if world > 1 else "single GPU"},
             "achieved_GBps": round(gbps_step, 1),
             "cg_iters_per_step": iters,
             "cg_iter_ms": round(cg_iter_ms, 4),

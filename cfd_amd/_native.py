@@ -137,6 +137,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_comm_destroy", None, V)
     _sig(lib, "hip_proj_comm_rank", C.c_int, V)
     _sig(lib, "hip_proj_comm_size", C.c_int, V)
+    _sig(lib, "hip_proj_comm_device_allreduce", C.c_int, V)
     _sig(lib, "hip_proj_create_slab", V, C.c_size_t, C.c_size_t, C.c_size_t, V,
          P(A.HipProjConfig))
     _sig(lib, "hip_proj_slab_info", C.c_int, V, P(C.c_size_t), P(C.c_size_t), P(C.c_int),

@@ -320,6 +320,10 @@ class SlabComm:
     def size(self) -> int:
         return _native.hip().hip_proj_comm_size(self._h)
 
+    @property
+    def device_allreduce(self) -> bool:
+        return bool(_native.hip().hip_proj_comm_device_allreduce(self._h))
+
     def close(self):
         if getattr(self, "_h", None):
             _native.hip().hip_proj_comm_destroy(self._h)

@@ -475,6 +475,9 @@ void hip_proj_comm_destroy(hip_proj_comm_t* c) {
 }
 
 int hip_proj_comm_rank(const hip_proj_comm_t* c) { return c && c->impl ? c->impl->rank : -1; }
+int hip_proj_comm_device_allreduce(const hip_proj_comm_t* c) {
+    return (c && c->impl && c->impl->device_mailbox()) ? 1 : 0;
+}
 int hip_proj_comm_size(const hip_proj_comm_t* c) { return c && c->impl ? c->impl->size : 0; }
 
 }  // extern "C"

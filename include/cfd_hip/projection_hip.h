@@ -204,6 +204,10 @@ CFD_HIP_EXPORT hip_proj_comm_t* hip_proj_comm_create_local(hip_proj_group_t* gro
 CFD_HIP_EXPORT void hip_proj_comm_destroy(hip_proj_comm_t* comm);
 CFD_HIP_EXPORT int hip_proj_comm_rank(const hip_proj_comm_t* comm);
 CFD_HIP_EXPORT int hip_proj_comm_size(const hip_proj_comm_t* comm);
+/* 1 when the CG dot products go through the one-shot peer-memory all-reduce
+ * (RCCL communicators; verified at creation, CFD_HIP_DEVICE_ALLREDUCE=0 turns it
+ * off), 0 when they use ncclAllReduce / the in-process group. */
+CFD_HIP_EXPORT int hip_proj_comm_device_allreduce(const hip_proj_comm_t* comm);
 /* Slab context for rank comm_rank of the global nx*ny*nz grid (3-D only). The
  * communicator must outlive the context. */
 CFD_HIP_EXPORT hip_proj_ctx_t* hip_proj_create_slab(size_t nx, size_t ny, size_t nz,

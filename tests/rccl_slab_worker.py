@@ -60,6 +60,9 @@ def main():
     dist.broadcast_object_list(uid, src=0)
     comm = api.SlabComm.rccl(uid[0], RANK, WORLD, 0)
     assert comm.rank == RANK and comm.size == WORLD
+    want_mb = os.environ.get("CFD_HIP_DEVICE_ALLREDUCE", "1") != "0"
+    if comm.device_allreduce != want_mb:
+        raise SystemExit(f"device all-reduce active={comm.device_allreduce}, expected {want_mb}")
 
     def cavity_bc(c):
         c.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
