@@ -34,10 +34,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh + prof_summary.py):
 # 2*FETCH_SIZE + WRITE_SIZE per working launch of sweep A, the gfx950
 # correction of MI355X_MICROARCH.md "HBM [CDNA4]".
-TRAFFIC_JSON = ROOT / "profiles" / "r01b_traffic_cg_sweeps.json"
-# Algorithmic HBM bytes per interior cell (DESIGN.md §4):
-BYTES_SWEEP_A = 40.0    # read r, p_old, x; write p_new, x
-BYTES_SWEEP_B = 24.0    # read p, r; write r
+TRAFFIC_JSON = ROOT / "profiles" / "r01c_traffic_cg_sweeps.json"
+# Algorithmic HBM bytes per interior cell (DESIGN.md §3):
+BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
+BYTES_SWEEP_B = 24.0    # even iterations: read p, r; write r
+BYTES_SWEEP_BX = 48.0   # odd iterations: + read x, p_prev; write x (two alpha p folded)
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
 BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
 
@@ -57,8 +58,9 @@ def parse():
                     help="CG iterations timed in the CPU baseline sample")
     ap.add_argument("--kchunk", type=int, default=0)
     ap.add_argument("--sweep-rows", type=int, default=16)
-    ap.add_argument("--sweep-variant", type=int, default=3,
-                    help="CG sweep memory hints: 1 NT stores, 2 NT loads, 3 both")
+    ap.add_argument("--sweep-variant", type=int, default=7,
+                    help="CG sweep variant: bit0 NT stores, bit1 NT loads, bit2 plane prefetch "
+                         "(built: 0-4, 7)")
     return ap.parse_args()
 
 
@@ -170,16 +172,27 @@ def main():
     gbps_step = step_bytes * args.steps / elapsed / 1e9
 
     kt = ctx.timing()
-    ms_a, n_a = kt["cg_sweep_a"]
-    ms_b, n_b = kt["cg_sweep_b"]
-    avg_a = ms_a / max(n_a, 1)
-    avg_b = ms_b / max(n_b, 1)
-    ach_a = BYTES_SWEEP_A * n_loc / (avg_a * 1e-3) / 1e9 if n_a else None
-    ach_b = BYTES_SWEEP_B * n_loc / (avg_b * 1e-3) / 1e9 if n_b else None
+    sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s)
+    for key, kname, bpc in (
+            ("cg_sweep_a", f"k_cgA<{args.sweep_rows}, false, {'true' if world > 1 else 'false'}, "
+                           f"{args.sweep_variant}>", BYTES_SWEEP_A),
+            ("cg_sweep_b", f"k_cgB<{args.sweep_rows}, {'true' if world > 1 else 'false'}, "
+                           f"{args.sweep_variant}, false>", BYTES_SWEEP_B),
+            ("cg_sweep_bx", f"k_cgB<{args.sweep_rows}, {'true' if world > 1 else 'false'}, "
+                            f"{args.sweep_variant}, true>", BYTES_SWEEP_BX)):
+        ms, cnt = kt[key]
+        avg = ms / cnt if cnt else None
+        ach = bpc * n_loc / (avg * 1e-3) / 1e9 if cnt else None
+        sweeps[key] = (kname, bpc, avg, cnt, ach, ms)
+    # one CG iteration = sweep A + the mean of the two sweep B forms
+    avg_a = sweeps["cg_sweep_a"][2] or 0.0
+    nb = sweeps["cg_sweep_b"][3] + sweeps["cg_sweep_bx"][3]
+    avg_b = (sweeps["cg_sweep_b"][5] + sweeps["cg_sweep_bx"][5]) / nb if nb else 0.0
     cg_iter_ms = avg_a + avg_b
     cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_loc / (cg_iter_ms * 1e-3) / 1e9
-
-    kname = f"k_cgA<{args.sweep_rows}, false, false, {args.sweep_variant}>"
+    # roofline on the dominant sweep (largest total time)
+    dom = max(sweeps, key=lambda k: sweeps[k][5])
+    kname, bpc_dom, avg_dom, _, ach_dom, _ = sweeps[dom]
     traffic, traffic_src = pmc_traffic(kname, n_loc) if world == 1 else (None, None)
 
     cpu = None
@@ -212,19 +225,21 @@ def main():
             "cg_iters_per_step": iters,
             "cg_iter_ms": round(cg_iter_ms, 4),
             "cg_iter_GBps_survey80": round(cg_iter_gbps_survey, 1),
-            "roofline": {"bound": "hbm", "kernel": "k_cgA",
-                         "achieved": round(ach_a, 1) if ach_a else None,
+            "roofline": {"bound": "hbm", "kernel": kname,
+                         "achieved": round(ach_dom, 1) if ach_dom else None,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(ach_a / HBM_PEAK_GBPS, 4) if ach_a else None,
+                         "frac": round(ach_dom / HBM_PEAK_GBPS, 4) if ach_dom else None,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes": BYTES_SWEEP_A * n_loc,
-                         "bytes_per_cell": BYTES_SWEEP_A,
-                         "avg_launch_ms": round(avg_a, 4)},
+                         "algorithmic_bytes": bpc_dom * n_loc,
+                         "bytes_per_cell": bpc_dom,
+                         "avg_launch_ms": round(avg_dom, 4) if avg_dom else None},
             "kernels": {k: {"total_ms": round(v[0], 3), "launches": v[1],
                             "avg_ms": round(v[0] / v[1], 4) if v[1] else None}
                         for k, v in kt.items() if v[1]},
-            "sweep_b": {"achieved": round(ach_b, 1) if ach_b else None,
-                        "bytes_per_cell": BYTES_SWEEP_B},
+            "cg_sweeps": {k: {"kernel": v[0], "bytes_per_cell": v[1],
+                              "avg_ms": round(v[2], 4) if v[2] else None,
+                              "achieved_GBps": round(v[4], 1) if v[4] else None}
+                          for k, v in sweeps.items()},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

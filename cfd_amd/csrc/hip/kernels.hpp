@@ -61,7 +61,7 @@ struct Lap {
 // Device-resident CG state; written only by the finishing (last) workgroup.
 struct CgState {
     double rho;     // (r, r) of the current residual
-    double alpha;   // alpha of the most recent sweep A
+    double alpha[2];// alpha_j of iteration j at [j & 1] (the fold needs two)
     double beta;    // beta for the next sweep A
     double pAp;
     double res;     // current residual 2-norm
@@ -71,10 +71,11 @@ struct CgState {
     int iterations; // completed iterations (reference stats->iterations)
     int done;       // no further iteration may run
     int status;     // poisson_solver_status_t
-    int pending;    // x still lacks alpha * p of the last iteration
+    int nalpha;     // iterations whose alpha is valid (x must hold alpha_j p_j, j < nalpha)
+    int xdone;      // x holds alpha_j p_j for j < xdone (folded by sweep B)
     int max_iter;
     int check_interval;
-    int pad0, pad1;
+    int pad0;
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -221,11 +222,13 @@ __device__ __forceinline__ void fin_setup(CgState* st, double tot, double rel_to
     st->res = res0;
     st->tol = tol;
     st->abs_tol = abs_tol;
-    st->alpha = 0.0;
+    st->alpha[0] = 0.0;
+    st->alpha[1] = 0.0;
     st->beta = 0.0;
     st->pAp = 0.0;
     st->iterations = 0;
-    st->pending = 0;
+    st->nalpha = 0;
+    st->xdone = 0;
     st->max_iter = max_iter;
     st->check_interval = check_interval;
     if (res0 < abs_tol || max_iter <= 0) {     // :357-365
@@ -244,15 +247,16 @@ __device__ __forceinline__ void fin_A(CgState* st, double tot, int it) {
         st->done = 1;
         st->status = ST_STAGNATED;
         st->iterations = it + 1;
-        st->pending = 0;
     } else {
-        st->alpha = st->rho / tot;
-        st->pending = 1;
+        st->alpha[it & 1] = st->rho / tot;
+        st->nalpha = it + 1;
     }
 }
 
-// after (r, r): convergence test, rho breakdown, beta (linear_solver_cg.c:416-445)
-__device__ __forceinline__ void fin_B(CgState* st, double tot, int it) {
+// after (r, r): convergence test, rho breakdown, beta (linear_solver_cg.c:416-445).
+// fold: this sweep B also folded alpha_{it-1} p_{it-1} + alpha_it p_it into x.
+__device__ __forceinline__ void fin_B(CgState* st, double tot, int it, bool fold) {
+    if (fold) st->xdone = it + 1;
     double res = sqrt(tot);
     st->res = res;
     st->iterations = it + 1;
@@ -288,8 +292,8 @@ static __global__ void k_finish_setup(CgState* st, const double* tot, double rel
 static __global__ void k_finish_A(CgState* st, const double* tot, int it) {
     if (threadIdx.x == 0 && !st->done) fin_A(st, tot[0], it);
 }
-static __global__ void k_finish_B(CgState* st, const double* tot, int it) {
-    if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it);
+static __global__ void k_finish_B(CgState* st, const double* tot, int it, int fold) {
+    if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it, fold != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -468,37 +472,69 @@ __device__ __forceinline__ RowPair row_pair(const SGeo& g) {
     return c;
 }
 
+// Loads of one plane step are issued through a small "bundle": without
+// SW_PREFETCH the bundle of plane k is loaded at the top of iteration k (and
+// its centre loads are consumed in the same iteration); with SW_PREFETCH the
+// bundle of plane k+1 is issued before plane k is processed, so one plane of
+// loads stays in flight across the LDS barrier and the arithmetic.
+constexpr int SW_PREFETCH = 4;
+
+__device__ __forceinline__ double2 fma2p(double2 a, double beta, double2 b) {
+    return make_double2(a.x + beta * b.x, a.y + beta * b.y);
+}
+
 // Sweep A (iteration it):  p_it = r + beta p_{it-1} (FIRST: p = r), written
-// to pnew; (p, A p) with A p in registers; deferred x += alpha_{it-1} p_{it-1}.
+// to pnew; (p, A p) with A p in registers. x is not touched here: sweep B of
+// every odd iteration folds the last two alpha p terms into x.
 template <int TY, bool FIRST, bool DIST, int FL = 0>
-static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const double* __restrict__ r,
-                                                 const double* __restrict__ po,
-                                                 double* __restrict__ pn, double* __restrict__ x,
-                                                 CgState* st, double* partials, unsigned* counter,
-                                                 int it, double* dsum, Mbox* mb) {
+static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_cgA(
+    SGeo g, Lap L, const double* __restrict__ r, const double* __restrict__ po,
+    double* __restrict__ pn, CgState* st, double* partials, unsigned* counter, int it,
+    double* dsum, Mbox* mb) {
+    constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
     const double beta = FIRST ? 0.0 : st->beta;
-    const double alpha = FIRST ? 0.0 : st->alpha;
     RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
     const int hslot = (c.w == 0) ? 0 : TY + 1;
     const long long hoff = (long long)(jh - min(c.j, g.ny - 1)) * g.px;
     const bool xok = c.i0 < g.nx;
-#define PV(ix) (FIRST ? ld2(r, ix) : [&] { double2 a_ = ld2(r, ix), b_ = ld2(po, ix); \
-        return make_double2(a_.x + beta * b_.x, a_.y + beta * b_.y); }())
-#define PS(ix) (FIRST ? r[ix] : (r[ix] + beta * po[ix]))
+    const bool eok_l = c.lane == 0 && c.i0 >= 1 && xok;
+    const bool eok_r = c.lane == 63 && c.i0 + 2 < g.nx;
+    const double2 zero = make_double2(0.0, 0.0);
+    // raw r / p_old of: the centre of plane k+1, the y-halo row of plane k+1,
+    // the x-edge cells of plane k (p is formed from them when used)
+    struct Bundle {
+        double2 cr, co, hr, ho;
+        double lr, lo, rr, ro;
+    };
+    auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
+        const double2 zero = make_double2(0.0, 0.0);  // a value, not the captured object
+        Bundle b;
+        const long long ip = ix + g.sz;
+        b.cr = xok ? ld2(r, ip) : zero;
+        b.co = (xok && !FIRST) ? ld2(po, ip) : zero;
+        const bool h = xok && halo && k + 1 < c.ke;
+        b.hr = h ? ld2(r, ip + hoff) : zero;
+        b.ho = (h && !FIRST) ? ld2(po, ip + hoff) : zero;
+        b.lr = eok_l ? r[ix - 1] : 0.0;
+        b.lo = (eok_l && !FIRST) ? po[ix - 1] : 0.0;
+        b.rr = eok_r ? r[ix + 2] : 0.0;
+        b.ro = (eok_r && !FIRST) ? po[ix + 2] : 0.0;
+        return b;
+    };
+    auto form2 = [&](double2 a, double2 b) { return FIRST ? a : fma2p(a, beta, b); };
+    auto form1 = [&](double a, double b) { return FIRST ? a : a + beta * b; };
     double acc = 0.0;
     long long idx = c.idx;
-    double2 zero = make_double2(0.0, 0.0);
-    double2 pm = xok ? PV(idx - g.sz) : zero;
-    double2 oc = (xok && !FIRST) ? ld2(po, idx) : zero;
-    double2 pc = xok ? (FIRST ? ld2(r, idx) : make_double2(ld2(r, idx).x + beta * oc.x,
-                                                          ld2(r, idx).y + beta * oc.y)) : zero;
-    double2 hc = (xok && halo) ? PV(idx + hoff) : zero;
+    double2 pm = xok ? form2(ld2(r, idx - g.sz), FIRST ? zero : ld2(po, idx - g.sz)) : zero;
+    double2 pc = xok ? form2(ld2(r, idx), FIRST ? zero : ld2(po, idx)) : zero;
+    double2 hc = (xok && halo) ? form2(ld2(r, idx + hoff), FIRST ? zero : ld2(po, idx + hoff))
+                               : zero;
     // Z-slabs: p is pointwise in r and p_old, so the tiles at the slab ends
     // also write the new p on the halo planes (r's halo is exchanged after
     // sweep B); sweep B then needs no halo exchange of p.
@@ -508,25 +544,26 @@ static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const dou
         pw.y = c.in1 ? pm.y : 0.0;
         st2(pn, idx - g.sz, pw);
     }
+    Bundle cur;
+    if (PF) cur = issue(c.kb, idx);
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-        const long long ip = idx + g.sz;
-        double2 op = (xok && !FIRST) ? ld2(po, ip) : zero;
-        double2 rp = xok ? ld2(r, ip) : zero;
-        double2 hp = (xok && halo && k + 1 < c.ke) ? PV(ip + hoff) : zero;
-        double2 xo = (xok && !FIRST) ? ld2v<FL>(x, idx) : zero;
-        double el = (c.lane == 0 && c.i0 >= 1 && xok) ? PS(idx - 1) : 0.0;
-        double er = (c.lane == 63 && c.i0 + 2 < g.nx) ? PS(idx + 2) : 0.0;
+        Bundle nxt;
+        if (PF) {
+            if (k + 1 < c.ke) nxt = issue(k + 1, idx + g.ps);
+        } else {
+            cur = issue(k, idx);
+        }
         rows[buf][c.w + 1][c.lane] = pc;
         if (halo) rows[buf][hslot][c.lane] = hc;
         __syncthreads();
         const double2 ys = rows[buf][c.w][c.lane];
         const double2 yn = rows[buf][c.w + 2][c.lane];
-        const double2 pp = FIRST ? rp : make_double2(rp.x + beta * op.x, rp.y + beta * op.y);
+        const double2 pp = form2(cur.cr, cur.co);
         double left = __shfl_up(pc.y, 1, 64);
         double right = __shfl_down(pc.x, 1, 64);
-        if (c.lane == 0) left = el;
-        if (c.lane == 63) right = er;
+        if (c.lane == 0) left = form1(cur.lr, cur.lo);
+        if (c.lane == 63) right = form1(cur.rr, cur.ro);
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
         if (c.act) {
@@ -534,19 +571,13 @@ static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const dou
             pw.x = c.in0 ? pc.x : 0.0;
             pw.y = c.in1 ? pc.y : 0.0;
             st2v<FL>(pn, idx, pw);
-            if (!FIRST) {
-                double2 xw;
-                xw.x = c.in0 ? xo.x + alpha * oc.x : xo.x;
-                xw.y = c.in1 ? xo.y + alpha * oc.y : xo.y;
-                st2v<FL>(x, idx, xw);
-            }
         }
         if (c.in0) acc += pc.x * Ap0;
         if (c.in1) acc += pc.y * Ap1;
         pm = pc;
         pc = pp;
-        oc = op;
-        hc = hp;
+        hc = form2(cur.hr, cur.ho);
+        if (PF) cur = nxt;
         buf ^= 1;
     }
     if (DIST && c.act && c.ke == g.k1) {  // pc = p on plane k1 (upper halo)
@@ -555,8 +586,6 @@ static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const dou
         pw.y = c.in1 ? pc.y : 0.0;
         st2(pn, idx, pw);
     }
-#undef PV
-#undef PS
     // deterministic workgroup sum: wave tree, then waves in order
     acc = wave_sum(acc);
     if (c.lane == 0) sh[c.w] = acc;
@@ -581,56 +610,94 @@ static __global__ __launch_bounds__(64 * TY) void k_cgA(SGeo g, Lap L, const dou
 
 // Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
 // to sweep A's), rho_new = (r, r), convergence test and beta.
-template <int TY, bool DIST, int FL = 0>
-static __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const double* __restrict__ p,
-                                                 double* __restrict__ r, CgState* st,
-                                                 double* partials, unsigned* counter, int it,
-                                                 double* dsum, Mbox* mb) {
+// FOLD (odd it): x = (x + alpha_{it-1} p_{it-1}) + alpha_it p_it, the
+// reference's two per-iteration updates x += alpha p (linear_solver_cg.c
+// :409-411) in their order, so x is bitwise the reference's while it is read
+// and written every other iteration only (p_{it-1} is the other p buffer).
+template <int TY, bool DIST, int FL = 0, bool FOLD = false>
+static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_cgB(
+    SGeo g, Lap L, const double* __restrict__ p, double* __restrict__ r,
+    const double* __restrict__ pprev, double* __restrict__ x, CgState* st, double* partials,
+    unsigned* counter, int it, double* dsum, Mbox* mb) {
+    constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
-    const double malpha = -st->alpha;
+    const double acur = st->alpha[it & 1];
+    const double aprev = FOLD ? st->alpha[(it + 1) & 1] : 0.0;
+    const double malpha = -acur;
     RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
     const int hslot = (c.w == 0) ? 0 : TY + 1;
     const long long hoff = (long long)(jh - min(c.j, g.ny - 1)) * g.px;
     const bool xok = c.i0 < g.nx;
+    const bool eok_l = c.lane == 0 && c.i0 >= 1 && xok;
+    const bool eok_r = c.lane == 63 && c.i0 + 2 < g.nx;
     const double2 zero = make_double2(0.0, 0.0);
+    // p of the centre and y-halo row of plane k+1; r, x, p_{it-1} and the
+    // x-edge p of plane k
+    struct Bundle {
+        double2 pp, hp, rr, xo, qo;
+        double el, er;
+    };
+    auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
+        const double2 zero = make_double2(0.0, 0.0);  // a value, not the captured object
+        Bundle b;
+        const long long ip = ix + g.sz;
+        b.pp = xok ? ld2(p, ip) : zero;
+        b.hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
+        b.rr = xok ? ld2v<FL>(r, ix) : zero;
+        b.xo = (FOLD && xok) ? ld2v<FL>(x, ix) : zero;
+        b.qo = (FOLD && xok) ? ld2v<FL>(pprev, ix) : zero;
+        b.el = eok_l ? p[ix - 1] : 0.0;
+        b.er = eok_r ? p[ix + 2] : 0.0;
+        return b;
+    };
     double acc = 0.0;
     long long idx = c.idx;
     double2 pm = xok ? ld2(p, idx - g.sz) : zero;
     double2 pc = xok ? ld2(p, idx) : zero;
     double2 hc = (xok && halo) ? ld2(p, idx + hoff) : zero;
+    Bundle cur;
+    if (PF) cur = issue(c.kb, idx);
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-        const long long ip = idx + g.sz;
-        double2 pp = xok ? ld2(p, ip) : zero;
-        double2 hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
-        double2 rr = xok ? ld2v<FL>(r, idx) : zero;
-        double el = (c.lane == 0 && c.i0 >= 1 && xok) ? p[idx - 1] : 0.0;
-        double er = (c.lane == 63 && c.i0 + 2 < g.nx) ? p[idx + 2] : 0.0;
+        Bundle nxt;
+        if (PF) {
+            if (k + 1 < c.ke) nxt = issue(k + 1, idx + g.ps);
+        } else {
+            cur = issue(k, idx);
+        }
         rows[buf][c.w + 1][c.lane] = pc;
         if (halo) rows[buf][hslot][c.lane] = hc;
         __syncthreads();
         const double2 ys = rows[buf][c.w][c.lane];
         const double2 yn = rows[buf][c.w + 2][c.lane];
+        const double2 pp = cur.pp;
         double left = __shfl_up(pc.y, 1, 64);
         double right = __shfl_down(pc.x, 1, 64);
-        if (c.lane == 0) left = el;
-        if (c.lane == 63) right = er;
+        if (c.lane == 0) left = cur.el;
+        if (c.lane == 63) right = cur.er;
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
         double2 rn;
-        rn.x = c.in0 ? rr.x + malpha * Ap0 : rr.x;
-        rn.y = c.in1 ? rr.y + malpha * Ap1 : rr.y;
+        rn.x = c.in0 ? cur.rr.x + malpha * Ap0 : cur.rr.x;
+        rn.y = c.in1 ? cur.rr.y + malpha * Ap1 : cur.rr.y;
         if (c.act) st2v<FL>(r, idx, rn);
+        if (FOLD && c.act) {
+            double2 xw;
+            xw.x = c.in0 ? (cur.xo.x + aprev * cur.qo.x) + acur * pc.x : cur.xo.x;
+            xw.y = c.in1 ? (cur.xo.y + aprev * cur.qo.y) + acur * pc.y : cur.xo.y;
+            st2v<FL>(x, idx, xw);
+        }
         if (c.in0) acc += rn.x * rn.x;
         if (c.in1) acc += rn.y * rn.y;
         pm = pc;
         pc = pp;
-        hc = hp;
+        hc = cur.hp;
+        if (PF) cur = nxt;
         buf ^= 1;
     }
     acc = wave_sum(acc);
@@ -646,24 +713,25 @@ static __global__ __launch_bounds__(64 * TY) void k_cgB(SGeo g, Lap L, const dou
         threadIdx.x == 0) {
         if (DIST && mb) {
             double g2;
-            if (mbox_allreduce(mb, tot, &g2)) fin_B(st, g2, it);
+            if (mbox_allreduce(mb, tot, &g2)) fin_B(st, g2, it, FOLD);
             else comm_fail(st);
         } else if (DIST) {
             dsum[0] = tot;
         } else {
-            fin_B(st, tot, it);
+            fin_B(st, tot, it, FOLD);
         }
     }
 }
 
-// Apply the deferred x += alpha p of the last iteration when the reference
-// would have applied it (converged, rho breakdown, max iterations).
+// Apply the x += alpha_j p_j the sweeps have not folded yet (j in [xdone,
+// nalpha): at most one, an even j, since every odd sweep B folds two).
 static __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, const double* __restrict__ p0,
                                                     const double* __restrict__ p1,
                                                     double* __restrict__ x, const CgState* st) {
-    if (!st->pending || st->iterations <= 0) return;
-    const double alpha = st->alpha;
-    const double* p = ((st->iterations - 1) & 1) ? p1 : p0;
+    if (st->xdone >= st->nalpha) return;
+    const int j = st->xdone;
+    const double alpha = st->alpha[j & 1];
+    const double* p = (j & 1) ? p1 : p0;
     const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         TileCoord c = tile_coord(g, t);

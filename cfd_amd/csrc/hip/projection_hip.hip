@@ -13,73 +13,85 @@
 
 template <int TY, bool FIRST, bool DIST, int FL>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
-                         double* pn, double* x, int it) {
+                         double* pn, int it) {
     hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST, FL>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
-                          c->stream, c->ta, c->tb, 0, c->sgeo, L, r, po, pn, x, c->st,
-                          c->partials, c->counter, it, c->dsum, mbox(c));
+                          c->stream, c->ta, c->tb, 0, c->sgeo, L, r, po, pn, c->st, c->partials,
+                          c->counter, it, c->dsum, mbox(c));
 }
 
-template <int TY, bool DIST, int FL>
-static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p,
-                         double* r, int it) {
+// Sweep B operands: p = p_it (stencil), r, and for the fold (odd it) p_{it-1}
+// and x.
+struct BArgs {
+    const double* p;
+    double* r;
+    const double* pprev;
+    double* x;
+};
+
+template <int TY, bool DIST, int FL, bool FOLD>
+static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
     const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
-    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(nb), dim3(64 * TY), 0, c->stream, c->ta,
-                          c->tb, 0, sg, L, p, r, c->st, c->partials, c->counter, it, c->dsum,
-                          mbox(c));
+    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, FOLD>), dim3(nb), dim3(64 * TY), 0, c->stream,
+                          c->ta, c->tb, 0, sg, L, a.p, a.r, a.pprev, a.x, c->st, c->partials,
+                          c->counter, it, c->dsum, mbox(c));
 }
 
 template <int TY, int FL>
 static void launch_cgA_f(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
-                         const double* po, double* pn, double* x, int it) {
+                         const double* po, double* pn, int it) {
     const bool d = dist(c);
-    if (first) d ? launch_cgA_t<TY, true, true, FL>(c, L, r, po, pn, x, it)
-                 : launch_cgA_t<TY, true, false, FL>(c, L, r, po, pn, x, it);
-    else d ? launch_cgA_t<TY, false, true, FL>(c, L, r, po, pn, x, it)
-           : launch_cgA_t<TY, false, false, FL>(c, L, r, po, pn, x, it);
+    if (first) d ? launch_cgA_t<TY, true, true, FL>(c, L, r, po, pn, it)
+                 : launch_cgA_t<TY, true, false, FL>(c, L, r, po, pn, it);
+    else d ? launch_cgA_t<TY, false, true, FL>(c, L, r, po, pn, it)
+           : launch_cgA_t<TY, false, false, FL>(c, L, r, po, pn, it);
 }
 
 template <int TY, int FL>
-static void launch_cgB_f(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p,
-                         double* r, int it) {
-    dist(c) ? launch_cgB_t<TY, true, FL>(c, sg, L, p, r, it)
-            : launch_cgB_t<TY, false, FL>(c, sg, L, p, r, it);
+static void launch_cgB_f(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
+    const bool fold = (it & 1) != 0;
+    if (dist(c)) fold ? launch_cgB_t<TY, true, FL, true>(c, sg, L, a, it)
+                      : launch_cgB_t<TY, true, FL, false>(c, sg, L, a, it);
+    else fold ? launch_cgB_t<TY, false, FL, true>(c, sg, L, a, it)
+              : launch_cgB_t<TY, false, FL, false>(c, sg, L, a, it);
 }
 
 template <int TY>
 static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
-                         const double* po, double* pn, double* x, int it) {
+                         const double* po, double* pn, int it) {
     switch (c->sweep_variant) {
-        case 1: return launch_cgA_f<TY, 1>(c, first, L, r, po, pn, x, it);
-        case 2: return launch_cgA_f<TY, 2>(c, first, L, r, po, pn, x, it);
-        case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, x, it);
-        default: return launch_cgA_f<TY, 0>(c, first, L, r, po, pn, x, it);
+        case 1: return launch_cgA_f<TY, 1>(c, first, L, r, po, pn, it);
+        case 2: return launch_cgA_f<TY, 2>(c, first, L, r, po, pn, it);
+        case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, it);
+        case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it);
+        case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it);
+        default: return launch_cgA_f<TY, 0>(c, first, L, r, po, pn, it);
     }
 }
 
 template <int TY>
-static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p,
-                         double* r, int it) {
+static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
     switch (c->sweep_variant) {
-        case 1: return launch_cgB_f<TY, 1>(c, sg, L, p, r, it);
-        case 2: return launch_cgB_f<TY, 2>(c, sg, L, p, r, it);
-        case 3: return launch_cgB_f<TY, 3>(c, sg, L, p, r, it);
-        default: return launch_cgB_f<TY, 0>(c, sg, L, p, r, it);
+        case 1: return launch_cgB_f<TY, 1>(c, sg, L, a, it);
+        case 2: return launch_cgB_f<TY, 2>(c, sg, L, a, it);
+        case 3: return launch_cgB_f<TY, 3>(c, sg, L, a, it);
+        case 4: return launch_cgB_f<TY, 4>(c, sg, L, a, it);
+        case 7: return launch_cgB_f<TY, 7>(c, sg, L, a, it);
+        default: return launch_cgB_f<TY, 0>(c, sg, L, a, it);
     }
 }
 
 // sweep_ty 8 or 16 (any sweep_variant), 4 (variant 0 only)
 static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
-                       const double* po, double* pn, double* x, int it) {
-    if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, x, it);
-    if (c->sweep_ty == 16) return launch_cgA_v<16>(c, first, L, r, po, pn, x, it);
-    return launch_cgA_v<8>(c, first, L, r, po, pn, x, it);
+                       const double* po, double* pn, int it) {
+    if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, it);
+    if (c->sweep_ty == 16) return launch_cgA_v<16>(c, first, L, r, po, pn, it);
+    return launch_cgA_v<8>(c, first, L, r, po, pn, it);
 }
 
-static void launch_cgB(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const double* p, double* r,
-                       int it) {
-    if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, sg, L, p, r, it);
-    if (c->sweep_ty == 16) return launch_cgB_v<16>(c, sg, L, p, r, it);
-    return launch_cgB_v<8>(c, sg, L, p, r, it);
+static void launch_cgB(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
+    if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, sg, L, a, it);
+    if (c->sweep_ty == 16) return launch_cgB_v<16>(c, sg, L, a, it);
+    return launch_cgB_v<8>(c, sg, L, a, it);
 }
 
 // ---------------------------------------------------------------------------
@@ -136,32 +148,32 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     auto iterate = [&](int it) -> cfd_status_t {
         double* pnew = P[it & 1];
         double* pold = P[(it + 1) & 1];
-        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, x, it); },
-              it);
+        const BArgs ba{pnew, c->r, pold, x};
+        const int kb = (it & 1) ? HIP_KT_CG_SWEEP_BX : HIP_KT_CG_SWEEP_B;
+        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, it); }, it);
         if (D && !mbox(c)) {
             ST_TRY(reduce_dot(c));
             hipExtLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
         }
-        if (!D) timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sgeo, L, pnew, c->r, it); }, it);
+        if (!D) timed(c, kb, [&] { launch_cgB(c, c->sgeo, L, ba, it); }, it);
         if (D) {
             // r's halo goes out on the side stream (halo communicator) as soon
             // as the two slab-edge planes of the new r exist: sweep B runs them
             // first, then the interior planes overlap the exchange; the (r,r)
             // all-reduce follows on the main stream; the next sweep A waits
             // for both
-            if (c->split_b) launch_cgB(c, c->sg_edge, L, pnew, c->r, it);
-            else timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sgeo, L, pnew, c->r, it); }, it);
+            if (c->split_b) launch_cgB(c, c->sg_edge, L, ba, it);
+            else timed(c, kb, [&] { launch_cgB(c, c->sgeo, L, ba, it); }, it);
             HIP_TRY(hipEventRecord(c->ev_b, c->stream));
             HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
             double* rr[1] = {c->r};
             ST_TRY(c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false));
             HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
-            if (c->split_b)
-                timed(c, HIP_KT_CG_SWEEP_B, [&] { launch_cgB(c, c->sg_int, L, pnew, c->r, it); }, it);
+            if (c->split_b) timed(c, kb, [&] { launch_cgB(c, c->sg_int, L, ba, it); }, it);
             if (!mbox(c)) {
                 ST_TRY(reduce_dot(c));
                 hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
-                                      c->st, c->dsum + 1, it);
+                                      c->st, c->dsum + 1, it, it & 1);
             }
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
         }
@@ -392,7 +404,7 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.kchunk = 0;
     c.verbose = 0;
     c.sweep_rows = 16;   // tools/sweep_bench.py at 512^3: 16 rows + NT hints fastest
-    c.sweep_variant = SW_NT_STORE | SW_NT_LOAD;
+    c.sweep_variant = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH;  // r01c sweep_bench at 512^3
     return c;
 }
 
@@ -467,7 +479,10 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
 
     // row-pair CG sweeps: 128 x TY x kc tiles (kernels.hpp, k_cgA / k_cgB)
     c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
-    c->sweep_variant = c->cfg.sweep_variant & 3;
+    {   // variants built: 0-3 (memory hints), 4 and 7 (+ plane prefetch)
+        const int v = c->cfg.sweep_variant & 7;
+        c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : v;
+    }
     SGeo& sg = c->sgeo;
     sg.nx = g.nx;
     sg.ny = g.ny;

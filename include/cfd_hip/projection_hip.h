@@ -61,7 +61,8 @@ typedef struct {
     int sweep_rows;               /* y rows (wavefronts) per CG sweep workgroup: 4, 8 or 16
                                      (default 16) */
     int sweep_variant;            /* CG sweep memory hints: bit0 non-temporal stores,
-                                     bit1 non-temporal loads of single-use inputs (default 3) */
+                                     bit1 non-temporal loads of single-use inputs, bit2 loads
+                                     issued one plane ahead (built: 0-3, 4, 7; default 7) */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
@@ -80,14 +81,15 @@ typedef enum {
 typedef enum {
     HIP_KT_PREDICTOR = 0,
     HIP_KT_CG_SETUP = 1,
-    HIP_KT_CG_SWEEP_A = 2, /* p = r + beta p, Ap on the fly, (p,Ap), deferred x += alpha p */
-    HIP_KT_CG_SWEEP_B = 3, /* r -= alpha A p (Ap recomputed), (r,r) */
+    HIP_KT_CG_SWEEP_A = 2, /* p = r + beta p, Ap on the fly, (p,Ap) */
+    HIP_KT_CG_SWEEP_B = 3, /* even iterations: r -= alpha A p (Ap recomputed), (r,r) */
     HIP_KT_CORRECTOR = 4,
     HIP_KT_RELAX = 5,      /* one RB-SOR colour pass or one Jacobi sweep */
     HIP_KT_RESIDUAL = 6,   /* L-infinity residual for the relaxation methods */
     HIP_KT_ENERGY = 7,     /* energy equation (alpha > 0) */
     HIP_KT_RK_STAGE = 8,   /* one fused RK4 stage (RHS + stage update) */
-    HIP_KT_COUNT = 9
+    HIP_KT_CG_SWEEP_BX = 9,/* odd iterations: sweep B + x += alpha p of both iterations */
+    HIP_KT_COUNT = 10
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);

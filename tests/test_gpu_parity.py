@@ -176,6 +176,46 @@ def test_poisson_cg_vs_oracle(hip_lib, n, expected):
     ctx.close()
 
 
+@pytest.mark.parametrize("iters", [1, 2, 3, 4, 5, 6])
+def test_poisson_cg_fixed_iterations_vs_oracle(hip_lib, iters):
+    """CG stopped by max_iterations after an odd or even count: sweep B folds
+    x every other iteration and the finalize kernel applies the last unfolded
+    alpha p, so x must hold exactly `iters` updates (linear_solver_cg.c:409-411)."""
+    g, rhs = cases.cos_rhs(17)
+    prm = oracle.poisson_params(max_iterations=iters)
+    xo = np.zeros_like(rhs)
+    so, sto = oracle.cg_solve(xo, rhs, g.dx, g.dy, g.dz, prm)
+    ctx = api.HipProjection(17, 17, 17)
+    xh = np.zeros_like(rhs)
+    sh, sth = ctx.poisson_solve(A.HIP_POISSON_CG, xh, rhs, g.dx, g.dy, g.dz, prm)
+    ctx.close()
+    assert sh == so
+    assert sth.iterations == sto.iterations == iters
+    assert _rel_maxdiff(xh, xo) < 1e-12
+
+
+@pytest.mark.parametrize("rows", [8, 16])
+def test_cg_sweep_variants_bitwise_equal(hip_lib, rows):
+    """The sweep variants (memory hints, plane prefetch) change how bytes move,
+    not the arithmetic or the reduction tree: bitwise equal solutions and
+    iteration counts for one tile height, and within the CG gate of the oracle."""
+    g, rhs = cases.cos_rhs(33)
+    xo = np.zeros_like(rhs)
+    oracle.cg_solve(xo, rhs, g.dx, g.dy, g.dz)
+    outs = []
+    for v in (0, 3, 4, 7):
+        ctx = api.HipProjection(33, 33, 33, sweep_rows=rows, sweep_variant=v)
+        xh = np.zeros_like(rhs)
+        sh, sth = ctx.poisson_solve(A.HIP_POISSON_CG, xh, rhs, g.dx, g.dy, g.dz)
+        ctx.close()
+        assert sh == A.CFD_SUCCESS
+        outs.append((sth.iterations, xh))
+    for it, xh in outs[1:]:
+        assert it == outs[0][0]
+        np.testing.assert_array_equal(xh, outs[0][1])
+    assert _rel_maxdiff(outs[0][1], xo) < 1e-9
+
+
 @pytest.mark.parametrize("method", [A.HIP_POISSON_REDBLACK, A.HIP_POISSON_JACOBI])
 def test_poisson_relax_bitwise(hip_lib, method):
     g, rhs = cases.cos_rhs(17)

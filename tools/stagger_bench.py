@@ -41,11 +41,14 @@ def main():
         ctx.close()
         a = kt["cg_sweep_a"]
         b = kt["cg_sweep_b"]
+        bx = kt["cg_sweep_bx"]
         cells = (n - 2) ** 3
         out = {("variant" if variants else "stagger"): st, "iter_us": round(ms / 100 * 1e3, 1),
                "A_us": round(a[0] / a[1] * 1e3, 1), "B_us": round(b[0] / b[1] * 1e3, 1),
-               "A_GBps": round(40 * cells / (a[0] / a[1] * 1e-3) / 1e9, 1),
-               "B_GBps": round(24 * cells / (b[0] / b[1] * 1e-3) / 1e9, 1)}
+               "BX_us": round(bx[0] / bx[1] * 1e3, 1),
+               "A_GBps": round(24 * cells / (a[0] / a[1] * 1e-3) / 1e9, 1),
+               "B_GBps": round(24 * cells / (b[0] / b[1] * 1e-3) / 1e9, 1),
+               "BX_GBps": round(48 * cells / (bx[0] / bx[1] * 1e-3) / 1e9, 1)}
         print(json.dumps(out), flush=True)
 
 

@@ -36,13 +36,13 @@ def main():
         kt = ctx.timing()
         ctx.enable_timing(False)
         ctx.close()
-        a, b = kt["cg_sweep_a"], kt["cg_sweep_b"]
-        ua, ub = a[0] / a[1] * 1e3, b[0] / b[1] * 1e3
+        a, b, bx = kt["cg_sweep_a"], kt["cg_sweep_b"], kt["cg_sweep_bx"]
+        ua, ub, ubx = (t[0] / t[1] * 1e3 for t in (a, b, bx))
         print(json.dumps({"cfg": spec, "iter_us": round(ms / iters * 1e3, 1),
-                          "A_us": round(ua, 1), "B_us": round(ub, 1),
-                          "A_GBps": round(40 * cells / (ua * 1e-6) / 1e9, 1),
-                          "B_GBps": round(24 * cells / (ub * 1e-6) / 1e9, 1)}), flush=True)
-
+                          "A_us": round(ua, 1), "B_us": round(ub, 1), "BX_us": round(ubx, 1),
+                          "A_GBps": round(24 * cells / (ua * 1e-6) / 1e9, 1),
+                          "B_GBps": round(24 * cells / (ub * 1e-6) / 1e9, 1),
+                          "BX_GBps": round(48 * cells / (ubx * 1e-6) / 1e9, 1)}), flush=True)
 
 if __name__ == "__main__":
     main()
