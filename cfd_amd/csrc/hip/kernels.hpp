@@ -612,7 +612,7 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
 // to sweep A's), rho_new = (r, r), convergence test and beta.
 // FOLD (odd it): x = (x + alpha_{it-1} p_{it-1}) + alpha_it p_it, the
 // reference's two per-iteration updates x += alpha p (linear_solver_cg.c
-// :409-411) in their order, so x is bitwise the reference's while it is read
+// :379-380, axpy :85-96) in their order, so x is bitwise the reference's while it is read
 // and written every other iteration only (p_{it-1} is the other p buffer).
 template <int TY, bool DIST, int FL = 0, bool FOLD = false>
 static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_cgB(

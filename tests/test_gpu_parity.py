@@ -180,7 +180,7 @@ def test_poisson_cg_vs_oracle(hip_lib, n, expected):
 def test_poisson_cg_fixed_iterations_vs_oracle(hip_lib, iters):
     """CG stopped by max_iterations after an odd or even count: sweep B folds
     x every other iteration and the finalize kernel applies the last unfolded
-    alpha p, so x must hold exactly `iters` updates (linear_solver_cg.c:409-411)."""
+    alpha p, so x must hold exactly `iters` updates (linear_solver_cg.c:379-380)."""
     g, rhs = cases.cos_rhs(17)
     prm = oracle.poisson_params(max_iterations=iters)
     xo = np.zeros_like(rhs)
