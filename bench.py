@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cg-iters", type=int, default=100,
                     help="CG iterations timed in the CPU baseline sample")
+    ap.add_argument("--cpu-scalar-cg-iters", type=int, default=5,
+                    help="CG iterations in the 1-thread CPU sample (0: skip it)")
     ap.add_argument("--kchunk", type=int, default=0)
     ap.add_argument("--sweep-rows", type=int, default=16)
     ap.add_argument("--sweep-variant", type=int, default=7,
@@ -195,6 +197,13 @@ def main():
     kname, bpc_dom, avg_dom, _, ach_dom, _ = sweeps[dom]
     traffic, traffic_src = pmc_traffic(kname, n_loc) if world == 1 else (None, None)
 
+    # measured HBM roof of this GPU (same library, 16-B lanes), after the
+    # timed region
+    import ctypes as C
+    cg, tr = C.c_double(0.0), C.c_double(0.0)
+    if lib.cfd_hip_stream_bench(local, 1 << 27, 5, C.byref(cg), C.byref(tr)) != A.CFD_SUCCESS:
+        cg.value = tr.value = 0.0
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
         cpu = cpu_baseline(n, args, k_mean)
@@ -232,7 +241,11 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": bpc_dom * n_loc,
                          "bytes_per_cell": bpc_dom,
-                         "avg_launch_ms": round(avg_dom, 4) if avg_dom else None},
+                         "avg_launch_ms": round(avg_dom, 4) if avg_dom else None,
+                         "stream_copy_GBps": round(cg.value, 1) or None,
+                         "stream_triad_GBps": round(tr.value, 1) or None,
+                         "frac_of_stream_copy": (round(ach_dom / cg.value, 4)
+                                                 if ach_dom and cg.value else None)},
             "kernels": {k: {"total_ms": round(v[0], 3), "launches": v[1],
                             "avg_ms": round(v[0] / v[1], 4) if v[1] else None}
                         for k, v in kt.items() if v[1]},
@@ -281,28 +294,42 @@ def cpu_baseline(n, args, k_gpu):
     except Exception:
         threads = os.cpu_count() or 1
     threads = max(1, min(threads, 64))
-    oracle.set_threads(threads)
     g = api.Grid(n, n, n, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
-    f = api.FlowField(n, n, n)
-    f.rho[...] = 1.0
-    api.cavity_bc(f, 1.0)
     p = api.validation_params(args.dt, 1.0 / args.re)
-    oracle.lib().oracle_set_poisson_cap(args.cpu_cg_iters)
-    t0 = time.perf_counter()
-    s, _, it = oracle.projection_step(f, g, p)
-    wall = time.perf_counter() - t0
-    oracle.lib().oracle_set_poisson_cap(0)
-    ph = oracle.last_phase_ms()
-    t_cg_iter = ph[2] / max(it, 1) / 1e3
-    t_step = (ph[0] + ph[1] + ph[3]) / 1e3 + k_gpu * t_cg_iter
     n_int = (n - 2) ** 3
-    return {"value": round(n_int / t_step / 1e6, 4), "unit": "MLUPS", "cores": threads,
-            "kind": "port",
-            "sample": (f"{n}^3 cavity step 1 on the host: predictor+divergence+corrector timed "
-                       f"in full, {it} CG iterations timed ({t_cg_iter*1e3:.1f} ms/iter) and "
-                       f"scaled to the GPU's {k_gpu:.0f} iterations/step; OpenMP x{threads}; "
-                       f"sample wall {wall:.1f} s"),
-            "cg_iter_ms": round(t_cg_iter * 1e3, 2), "status": s}
+
+    def sample(nthreads, cg_iters):
+        oracle.set_threads(nthreads)
+        f = api.FlowField(n, n, n)
+        f.rho[...] = 1.0
+        api.cavity_bc(f, 1.0)
+        oracle.lib().oracle_set_poisson_cap(cg_iters)
+        t0 = time.perf_counter()
+        s, _, it = oracle.projection_step(f, g, p)
+        wall = time.perf_counter() - t0
+        oracle.lib().oracle_set_poisson_cap(0)
+        ph = oracle.last_phase_ms()
+        t_cg_iter = ph[2] / max(it, 1) / 1e3
+        t_step = (ph[0] + ph[1] + ph[3]) / 1e3 + k_gpu * t_cg_iter
+        return s, it, wall, t_cg_iter, t_step
+
+    s, it, wall, t_cg_iter, t_step = sample(threads, args.cpu_cg_iters)
+    out = {"value": round(n_int / t_step / 1e6, 4), "unit": "MLUPS", "cores": threads,
+           "kind": "port",
+           "sample": (f"{n}^3 cavity step 1 on the host: predictor+divergence+corrector timed "
+                      f"in full, {it} CG iterations timed ({t_cg_iter*1e3:.1f} ms/iter) and "
+                      f"scaled to the GPU's {k_gpu:.0f} iterations/step; OpenMP x{threads}; "
+                      f"sample wall {wall:.1f} s"),
+           "cg_iter_ms": round(t_cg_iter * 1e3, 2), "status": s}
+    if args.cpu_scalar_cg_iters > 0:
+        # the scalar reference configuration: one thread
+        s1, it1, wall1, t1_cg, t1_step = sample(1, args.cpu_scalar_cg_iters)
+        out["scalar_1core"] = {"value": round(n_int / t1_step / 1e6, 4), "unit": "MLUPS",
+                               "cores": 1, "cg_iter_ms": round(t1_cg * 1e3, 1),
+                               "sample": f"same step, {it1} CG iterations timed, wall {wall1:.1f} s",
+                               "status": s1}
+    oracle.set_threads(threads)
+    return out
 
 
 if __name__ == "__main__":

@@ -160,6 +160,13 @@ CFD_HIP_EXPORT size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx);
 CFD_HIP_EXPORT double hip_proj_cg_fixed_iters(hip_proj_ctx_t* ctx, const double* rhs_host,
                                               double dx, double dy, double dz, int iters);
 
+/* Measurement helper (not a reference interface): BabelStream-style copy and
+ * triad over fp64 arrays of n elements with 16-B lanes on `device`; best of
+ * `reps` timed rounds, in GB/s (BabelStream byte counts). The measured HBM roof
+ * bench.py reports beside the 8 TB/s spec. */
+CFD_HIP_EXPORT cfd_status_t cfd_hip_stream_bench(int device, size_t n, int reps,
+                                                 double* copy_gbps, double* triad_gbps);
+
 /* Standalone pressure-Poisson solve on host buffers, the HIP counterpart of
  * poisson_solver_solve with a POISSON_BACKEND_GPU solver (linear_solver.c:487-509,
  * poisson_solver_cg_gpu.cu:135-178): upload x and rhs, solve lap(x) = rhs with

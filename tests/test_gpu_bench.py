@@ -51,17 +51,17 @@ def test_bench_one_gpu_contract(hip_lib):
     assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
 
 
-@pytest.mark.parametrize("case", ["cavity", "tg"])
-def test_bench_two_rank_rehearsal(hip_lib, case):
+@pytest.mark.parametrize("case,world", [("cavity", 2), ("tg", 2), ("cavity", 4)])
+def test_bench_multi_rank_rehearsal(hip_lib, case, world):
     env = _env()
     env["CFD_BENCH_SHARED_GPU"] = "1"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", str(world),
            "--size", "66", "--steps", "2", "--warmup", "1", "--case", case]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     d = _last_json(r.stdout)
     assert KEYS <= set(d)
-    assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "strong"
+    assert d["n_gpus"] == world and d["value"] > 0 and d["scaling"] == "strong"
     assert d["cpu_baseline"] is None  # CPU baseline at N=1 only
-    assert "z-slab x2" in d["config"]["parallelism"]
+    assert f"z-slab x{world}" in d["config"]["parallelism"]

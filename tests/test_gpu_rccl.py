@@ -18,16 +18,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("device_allreduce", ["0", "1"])
-def test_rccl_two_rank_slabs(hip_lib, device_allreduce):
+@pytest.mark.parametrize("world,device_allreduce", [(2, "0"), (2, "1"), (4, "1")])
+def test_rccl_slabs(hip_lib, world, device_allreduce):
     """device_allreduce=1 (the default): CG dots through the one-shot
-    peer-memory mailbox (IPC-mapped between the two processes, verified by a
-    collective probe at communicator creation); 0: ncclAllReduce."""
+    peer-memory mailbox (IPC-mapped between the processes, verified by a
+    collective probe at communicator creation); 0: ncclAllReduce. With 4
+    ranks the middle ranks exchange halos with two neighbours."""
     env = dict(os.environ)
     env["CFD_HIP_DEVICE_ALLREDUCE"] = device_allreduce
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            str(ROOT / "tests" / "rccl_slab_worker.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
