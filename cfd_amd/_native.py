@@ -94,6 +94,14 @@ def _bind_host(lib) -> None:
     _sig(lib, "free_simulation", None, P(A.SimulationData))
     _sig(lib, "run_simulation_step", C.c_int, P(A.SimulationData))
     _sig(lib, "run_simulation_solve", C.c_int, P(A.SimulationData))
+    _sig(lib, "cfd_checkpoint_write", C.c_int, C.c_char_p, P(A.Grid), P(A.FlowField),
+         P(A.SolverParams), C.c_double, C.c_char_p, C.c_char_p, C.c_char_p)
+    _sig(lib, "cfd_checkpoint_read", C.c_int, C.c_char_p, P(P(A.Grid)), P(P(A.FlowField)),
+         P(A.SolverParams), P(C.c_double), C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+         C.c_char_p, C.c_size_t)
+    _sig(lib, "save_simulation_checkpoint", C.c_int, P(A.SimulationData), C.c_char_p)
+    _sig(lib, "load_simulation_from_checkpoint", P(A.SimulationData), C.c_char_p)
+    _sig(lib, "restore_simulation_checkpoint", C.c_int, P(A.SimulationData), C.c_char_p)
 
 
 def _bind_hip(lib) -> None:

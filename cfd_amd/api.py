@@ -53,6 +53,13 @@ class Grid:
             raise CfdError(h.cfd_get_last_status(), "grid_create")
         h.grid_initialize_uniform(self._ptr)
 
+    @classmethod
+    def adopt(cls, ptr) -> "Grid":
+        """Take ownership of a grid* the C library allocated (grid_destroy frees it)."""
+        g = cls.__new__(cls)
+        g._ptr = ptr
+        return g
+
     @property
     def ptr(self):
         return self._ptr
@@ -112,11 +119,21 @@ class FlowField:
         self._ptr = h.flow_field_create(nx, ny, nz)
         if not self._ptr:
             raise CfdError(h.cfd_get_last_status(), "flow_field_create")
-        n = nx * ny * nz
-        shape = (nz, ny, nx)
+        self._bind_views()
+
+    def _bind_views(self):
         c = self._ptr.contents
+        n = c.nx * c.ny * c.nz
         for name in self.NAMES:
-            setattr(self, name, _view(getattr(c, name), n, shape))
+            setattr(self, name, _view(getattr(c, name), n, (c.nz, c.ny, c.nx)))
+
+    @classmethod
+    def adopt(cls, ptr) -> "FlowField":
+        """Take ownership of a flow_field* the C library allocated."""
+        f = cls.__new__(cls)
+        f._ptr = ptr
+        f._bind_views()
+        return f
 
     @property
     def ptr(self):
@@ -190,6 +207,35 @@ def cavity_bc(field: FlowField, lid: float = 1.0) -> None:
     (lid_driven_cavity_common.h:140-160 / SURVEY.md §8d config 3)."""
     bc_apply_dirichlet_velocity_3d(field, dirichlet(top=lid), dirichlet(), dirichlet())
     bc_apply_scalar_3d(field.p, A.BC_TYPE_NEUMANN)
+
+
+def checkpoint_write(path: str, grid: "Grid", field: "FlowField", params: A.SolverParams,
+                     time: float, solver_name: str, run_prefix: Optional[str] = None,
+                     base_dir: Optional[str] = None) -> int:
+    """cfd_checkpoint_write (checkpoint.h:49-75) through libcfd_host.so."""
+    enc = (lambda x: x.encode() if x is not None else None)
+    return _native.host().cfd_checkpoint_write(
+        path.encode(), grid.ptr if grid is not None else None,
+        field.ptr if field is not None else None,
+        C.byref(params) if params is not None else None, time, enc(solver_name),
+        enc(run_prefix), enc(base_dir))
+
+
+def checkpoint_read(path: str, caps=(128, 256, 512)):
+    """cfd_checkpoint_read (checkpoint.h:77-115): returns (status, Grid, FlowField,
+    params, time, solver_name, run_prefix, base_dir); cap 0 passes NULL."""
+    h = _native.host()
+    gp = C.POINTER(A.Grid)()
+    fp = C.POINTER(A.FlowField)()
+    prm = A.SolverParams()
+    t = C.c_double(0.0)
+    bufs = [C.create_string_buffer(c) if c else None for c in caps]
+    st = h.cfd_checkpoint_read(path.encode(), C.byref(gp), C.byref(fp), C.byref(prm),
+                               C.byref(t), bufs[0], caps[0], bufs[1], caps[1], bufs[2], caps[2])
+    if st != A.CFD_SUCCESS:
+        return st, None, None, prm, 0.0, None, None, None
+    return (st, Grid.adopt(gp), FlowField.adopt(fp), prm, t.value,
+            *[b.value.decode() if b is not None else None for b in bufs])
 
 
 class Registry:

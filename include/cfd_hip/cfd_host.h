@@ -13,7 +13,9 @@
  *   registry     lib/include/cfd/solvers/navier_stokes_solver.h:291-371,
  *                lib/src/api/solver_registry.c:202-494
  *   simulation   lib/include/cfd/api/simulation_api.h (init_simulation_with_solver,
- *                run_simulation_step, run_simulation_solve, free_simulation)
+ *                run_simulation_step, run_simulation_solve, free_simulation,
+ *                save/load/restore_simulation_checkpoint)
+ *   restart      lib/include/cfd/io/checkpoint.h (cfd_checkpoint_write/read)
  * cfd_registry_register_defaults registers the HIP projection solvers when
  * libcfd_hip.so is loaded in the process (it looks up cfd_hip_register_solvers).
  */
@@ -109,6 +111,27 @@ CFD_HIP_EXPORT void free_simulation(simulation_data* sim);
 CFD_HIP_EXPORT cfd_status_t run_simulation_step(simulation_data* sim);
 CFD_HIP_EXPORT cfd_status_t run_simulation_solve(simulation_data* sim);
 CFD_HIP_EXPORT const ns_solver_stats_t* simulation_get_stats(const simulation_data* sim);
+
+/* restart files (lib/include/cfd/io/checkpoint.h:49-115, simulation_api.h:93-111):
+ * the reference's `.cfdchk` format, status codes and ownership rules */
+CFD_HIP_EXPORT cfd_status_t cfd_checkpoint_write(const char* path, const grid* g,
+                                                 const flow_field* field,
+                                                 const ns_solver_params_t* params,
+                                                 double current_time, const char* solver_name,
+                                                 const char* run_prefix,
+                                                 const char* output_base_dir);
+CFD_HIP_EXPORT cfd_status_t cfd_checkpoint_read(const char* path, grid** out_grid,
+                                                flow_field** out_field,
+                                                ns_solver_params_t* out_params,
+                                                double* out_current_time, char* out_solver_name,
+                                                size_t solver_name_cap, char* out_run_prefix,
+                                                size_t run_prefix_cap, char* out_output_base_dir,
+                                                size_t output_base_dir_cap);
+CFD_HIP_EXPORT cfd_status_t save_simulation_checkpoint(const simulation_data* sim,
+                                                       const char* path);
+CFD_HIP_EXPORT simulation_data* load_simulation_from_checkpoint(const char* path);
+CFD_HIP_EXPORT cfd_status_t restore_simulation_checkpoint(simulation_data* sim,
+                                                          const char* path);
 
 #ifdef __cplusplus
 }
