@@ -126,6 +126,12 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_apply_scalar_bc", C.c_int, V, C.c_int, C.c_int)
     _sig(lib, "hip_proj_apply_dirichlet", C.c_int, V, C.c_int, P(A.DirichletValues))
     _sig(lib, "hip_proj_get_poisson_stats", C.c_int, V, P(A.PoissonStats))
+    _sig(lib, "hip_proj_field_crc32", C.c_int, V, C.c_int, P(C.c_uint32))
+    _sig(lib, "hip_proj_checkpoint_write", C.c_int, V, C.c_char_p, P(A.Grid), P(A.SolverParams),
+         C.c_double, C.c_char_p, C.c_char_p, C.c_char_p)
+    _sig(lib, "hip_proj_checkpoint_read", C.c_int, V, C.c_char_p, P(P(A.Grid)),
+         P(A.SolverParams), P(C.c_double), C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+         C.c_char_p, C.c_size_t)
     _sig(lib, "hip_proj_apply_thermal_bcs", C.c_int, V, P(A.SolverParams))
     _sig(lib, "hip_proj_enable_timing", None, V, C.c_int)
     _sig(lib, "hip_proj_reset_timing", None, V)

@@ -498,6 +498,34 @@ class HipProjection:
         _check(self._lib().hip_proj_set_field(self._ctx, fid, a.ctypes.data_as(A.c_double_p)),
                "hip_proj_set_field")
 
+    def field_crc32(self, fid: int) -> int:
+        """hip_proj_field_crc32: zlib CRC-32 of the packed field, computed on the GPU."""
+        v = C.c_uint32(0)
+        _check(self._lib().hip_proj_field_crc32(self._ctx, fid, C.byref(v)), "hip_proj_field_crc32")
+        return v.value
+
+    def checkpoint_write(self, path: str, grid: "Grid", params: A.SolverParams, time: float,
+                         solver_name: str, run_prefix: Optional[str] = None,
+                         base_dir: Optional[str] = None) -> int:
+        enc = (lambda x: x.encode() if x is not None else None)
+        return self._lib().hip_proj_checkpoint_write(
+            self._ctx, path.encode(), grid.ptr, C.byref(params), time, enc(solver_name),
+            enc(run_prefix), enc(base_dir))
+
+    def checkpoint_read(self, path: str, caps=(128, 256, 512)):
+        """(status, Grid, params, time, solver_name, run_prefix, base_dir)."""
+        gp = C.POINTER(A.Grid)()
+        prm = A.SolverParams()
+        t = C.c_double(0.0)
+        bufs = [C.create_string_buffer(c) if c else None for c in caps]
+        st = self._lib().hip_proj_checkpoint_read(self._ctx, path.encode(), C.byref(gp),
+                                                  C.byref(prm), C.byref(t), bufs[0], caps[0],
+                                                  bufs[1], caps[1], bufs[2], caps[2])
+        if st != A.CFD_SUCCESS:
+            return st, None, prm, 0.0, None, None, None
+        return (st, Grid.adopt(gp), prm, t.value,
+                *[b.value.decode() if b is not None else None for b in bufs])
+
     def get_field(self, fid: int) -> np.ndarray:
         out = np.empty(self.shape, dtype=np.float64)
         _check(self._lib().hip_proj_get_field(self._ctx, fid, out.ctypes.data_as(A.c_double_p)),

@@ -28,6 +28,8 @@
 
 #include "cfd_hip/cfd_abi.h"
 
+#include <stdint.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -159,6 +161,38 @@ CFD_HIP_EXPORT size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx);
  * iterations with no early exit. Returns elapsed device ms (events). */
 CFD_HIP_EXPORT double hip_proj_cg_fixed_iters(hip_proj_ctx_t* ctx, const double* rhs_host,
                                               double dx, double dy, double dz, int iters);
+
+/* Restart files of the device-resident state, in the reference's .cfdchk
+ * format (cfd_checkpoint_write / cfd_checkpoint_read, lib/include/cfd/io/
+ * checkpoint.h:49-115; same argument meaning, status codes and string-buffer
+ * rules). Fields stream between HBM and the file through pinned staging and
+ * their CRC-32 is computed on the GPU. write: g must match the context's
+ * dimensions; the fields written are the context's u, v, w, p, rho (rho0
+ * everywhere when no per-cell density was set), T (zeros when absent).
+ * read: the file's dimensions must equal the context's (CFD_ERROR_INVALID
+ * otherwise); the state is replaced only after the trailing CRC matched;
+ * *out_grid (may be NULL) receives a newly allocated grid, freed with
+ * grid_destroy. Single-device contexts only (Z-slab: CFD_ERROR_UNSUPPORTED). */
+CFD_HIP_EXPORT cfd_status_t hip_proj_checkpoint_write(hip_proj_ctx_t* ctx, const char* path,
+                                                      const grid* g,
+                                                      const ns_solver_params_t* params,
+                                                      double current_time,
+                                                      const char* solver_name,
+                                                      const char* run_prefix,
+                                                      const char* output_base_dir);
+CFD_HIP_EXPORT cfd_status_t hip_proj_checkpoint_read(hip_proj_ctx_t* ctx, const char* path,
+                                                     grid** out_grid,
+                                                     ns_solver_params_t* out_params,
+                                                     double* out_current_time,
+                                                     char* out_solver_name,
+                                                     size_t solver_name_cap,
+                                                     char* out_run_prefix, size_t run_prefix_cap,
+                                                     char* out_output_base_dir,
+                                                     size_t output_base_dir_cap);
+/* IEEE CRC-32 (zlib's) of one device field in the packed reference layout
+ * (idx = k*nx*ny + j*nx + i, little-endian doubles), computed on the GPU. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_field_crc32(hip_proj_ctx_t* ctx, int field_id,
+                                                 uint32_t* crc);
 
 /* Measurement helper (not a reference interface): BabelStream-style copy and
  * triad over fp64 arrays of n elements with 16-B lanes on `device`; best of
