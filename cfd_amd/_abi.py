@@ -137,6 +137,7 @@ class HipProjConfig(C.Structure):
         ("poisson_max_iter", C.c_int), ("poisson_check_interval", C.c_int),
         ("sor_omega", C.c_double), ("poll_interval", C.c_int), ("kchunk", C.c_int),
         ("verbose", C.c_int), ("sweep_rows", C.c_int), ("sweep_variant", C.c_int),
+        ("rhs_density", C.c_int), ("poisson_fail_fatal", C.c_int),
     ]
 
 
@@ -146,4 +147,59 @@ class SimulationData(C.Structure):
         ("solver", C.POINTER(NSSolver)), ("registry", C.c_void_p),
         ("last_stats", SolverStats), ("outputs", C.c_void_p), ("run_prefix", C.c_char_p),
         ("current_time", C.c_double), ("output_base_dir", C.c_char * 512),
+    ]
+
+
+# gpu_device.h:32-82 (include/cfd_hip/gpu_device.h)
+class GpuConfig(C.Structure):
+    _fields_ = [
+        ("enable_gpu", C.c_int), ("min_grid_size", C.c_size_t), ("min_steps", C.c_int),
+        ("block_size_x", C.c_int), ("block_size_y", C.c_int), ("poisson_max_iter", C.c_int),
+        ("poisson_tolerance", C.c_double), ("persistent_memory", C.c_int),
+        ("async_transfers", C.c_int), ("sync_after_kernel", C.c_int), ("verbose", C.c_int),
+    ]
+
+
+class GpuDeviceInfo(C.Structure):
+    _fields_ = [
+        ("device_id", C.c_int), ("name", C.c_char * 256), ("total_memory", C.c_size_t),
+        ("free_memory", C.c_size_t), ("compute_capability_major", C.c_int),
+        ("compute_capability_minor", C.c_int), ("multiprocessor_count", C.c_int),
+        ("max_threads_per_block", C.c_int), ("warp_size", C.c_int), ("is_available", C.c_int),
+    ]
+
+
+class GpuSolverStats(C.Structure):
+    _fields_ = [
+        ("kernel_time_ms", C.c_double), ("transfer_time_ms", C.c_double),
+        ("poisson_time_ms", C.c_double), ("poisson_iterations", C.c_int),
+        ("poisson_residual", C.c_double), ("memory_allocated", C.c_size_t),
+        ("kernels_launched", C.c_int),
+    ]
+
+
+# poisson_solver_method_t / poisson_solver_backend_t (poisson_solver.h)
+POISSON_METHOD_JACOBI = 0
+POISSON_METHOD_GAUSS_SEIDEL = 1
+POISSON_METHOD_SOR = 2
+POISSON_METHOD_REDBLACK_SOR = 3
+POISSON_METHOD_CG = 4
+POISSON_METHOD_BICGSTAB = 5
+POISSON_METHOD_MULTIGRID = 6
+POISSON_BACKEND_AUTO = 0
+POISSON_BACKEND_SCALAR = 1
+POISSON_BACKEND_OMP = 2
+POISSON_BACKEND_SIMD = 3
+POISSON_BACKEND_GPU = 4
+POISSON_ERROR = -1
+
+
+class PoissonSolver(C.Structure):
+    _fields_ = [
+        ("name", C.c_char_p), ("description", C.c_char_p), ("method", C.c_int),
+        ("backend", C.c_int), ("nx", C.c_size_t), ("ny", C.c_size_t), ("nz", C.c_size_t),
+        ("dx", C.c_double), ("dy", C.c_double), ("dz", C.c_double),
+        ("params", PoissonParams), ("context", C.c_void_p), ("init", C.c_void_p),
+        ("destroy", C.c_void_p), ("solve", C.c_void_p), ("iterate", C.c_void_p),
+        ("apply_bc", C.c_void_p),
     ]

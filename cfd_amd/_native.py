@@ -102,6 +102,17 @@ def _bind_host(lib) -> None:
     _sig(lib, "save_simulation_checkpoint", C.c_int, P(A.SimulationData), C.c_char_p)
     _sig(lib, "load_simulation_from_checkpoint", P(A.SimulationData), C.c_char_p)
     _sig(lib, "restore_simulation_checkpoint", C.c_int, P(A.SimulationData), C.c_char_p)
+    _sig(lib, "poisson_solver_params_default", A.PoissonParams)
+    _sig(lib, "poisson_solver_stats_default", A.PoissonStats)
+    _sig(lib, "poisson_solver_backend_available", C.c_bool, C.c_int)
+    _sig(lib, "poisson_solver_create", P(A.PoissonSolver), C.c_int, C.c_int)
+    _sig(lib, "poisson_solver_init", C.c_int, P(A.PoissonSolver), C.c_size_t, C.c_size_t,
+         C.c_size_t, C.c_double, C.c_double, C.c_double, P(A.PoissonParams))
+    _sig(lib, "poisson_solver_destroy", None, P(A.PoissonSolver))
+    _sig(lib, "poisson_solver_solve", C.c_int, P(A.PoissonSolver), A.c_double_p, A.c_double_p,
+         A.c_double_p, P(A.PoissonStats))
+    _sig(lib, "poisson_solver_iterate", C.c_int, P(A.PoissonSolver), A.c_double_p, A.c_double_p,
+         A.c_double_p, A.c_double_p)
 
 
 def _bind_hip(lib) -> None:
@@ -164,6 +175,29 @@ def _bind_hip(lib) -> None:
     _sig(lib, "create_projection_hip_solver", P(A.NSSolver))
     _sig(lib, "create_rk4_hip_solver", P(A.NSSolver))
     _sig(lib, "cfd_hip_register_solvers", None, V)
+    _sig(lib, "create_cg_gpu_solver", P(A.PoissonSolver))
+    _sig(lib, "create_redblack_gpu_solver", P(A.PoissonSolver))
+    _sig(lib, "create_jacobi_gpu_solver", P(A.PoissonSolver))
+    # gpu_device.h API
+    _sig(lib, "gpu_config_default", A.GpuConfig)
+    _sig(lib, "gpu_is_available", C.c_int)
+    _sig(lib, "gpu_get_device_info", C.c_int, P(A.GpuDeviceInfo), C.c_int)
+    _sig(lib, "gpu_select_device", C.c_int, C.c_int)
+    _sig(lib, "gpu_should_use", C.c_int, P(A.GpuConfig), C.c_size_t, C.c_size_t, C.c_size_t,
+         C.c_int)
+    _sig(lib, "gpu_solver_create", V, C.c_size_t, C.c_size_t, C.c_size_t, P(A.GpuConfig))
+    _sig(lib, "gpu_solver_destroy", None, V)
+    _sig(lib, "gpu_solver_upload", C.c_int, V, P(A.FlowField))
+    _sig(lib, "gpu_solver_download", C.c_int, V, P(A.FlowField))
+    _sig(lib, "gpu_solver_step", C.c_int, V, P(A.Grid), P(A.SolverParams), P(A.GpuSolverStats))
+    _sig(lib, "gpu_solver_get_stats", A.GpuSolverStats, V)
+    _sig(lib, "gpu_solver_reset_stats", None, V)
+    _sig(lib, "solve_navier_stokes_gpu", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
+         P(A.GpuConfig))
+    _sig(lib, "solve_projection_method_gpu", C.c_int, P(A.FlowField), P(A.Grid),
+         P(A.SolverParams), P(A.GpuConfig))
+    _sig(lib, "solve_rk4_method_gpu", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
+         P(A.GpuConfig))
 
 
 def _import_torch_first() -> None:

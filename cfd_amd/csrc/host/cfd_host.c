@@ -579,3 +579,105 @@ cfd_status_t run_simulation_solve(simulation_data* s) {
 const ns_solver_stats_t* simulation_get_stats(const simulation_data* s) {
     return s ? &s->last_stats : NULL;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Poisson solver interface (linear_solver.c:25-535), GPU backend only       */
+/* ------------------------------------------------------------------------ */
+poisson_solver_params_t poisson_solver_params_default(void) {
+    /* linear_solver.c:37-47 */
+    poisson_solver_params_t p;
+    memset(&p, 0, sizeof(p));
+    p.tolerance = 1e-6;
+    p.absolute_tolerance = 1e-10;
+    p.max_iterations = 5000;
+    p.omega = 0.0;
+    p.check_interval = 1;
+    p.verbose = false;
+    p.preconditioner = POISSON_PRECOND_NONE;
+    return p;
+}
+
+poisson_solver_stats_t poisson_solver_stats_default(void) {
+    /* linear_solver.c:49-57 */
+    poisson_solver_stats_t s;
+    memset(&s, 0, sizeof(s));
+    s.status = POISSON_ERROR;
+    return s;
+}
+
+static int hip_device_visible(void) {
+    int (*avail)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "hip_projection_available");
+    return avail ? avail() : 0;
+}
+
+bool poisson_solver_backend_available(poisson_solver_backend_t backend) {
+    /* linear_solver.c:105-131, for a library whose only solvers are the HIP ones */
+    if (backend == POISSON_BACKEND_GPU || backend == POISSON_BACKEND_AUTO)
+        return hip_device_visible() != 0;
+    return false;
+}
+
+poisson_solver_t* poisson_solver_create(poisson_solver_method_t method,
+                                        poisson_solver_backend_t backend) {
+    /* linear_solver.c:150-235: no silent fallbacks; NULL when the pair is absent */
+    if (backend == POISSON_BACKEND_AUTO) backend = POISSON_BACKEND_GPU;
+    if (backend != POISSON_BACKEND_GPU) return NULL;
+    const char* factory = NULL;
+    switch (method) {
+        case POISSON_METHOD_JACOBI: factory = "create_jacobi_gpu_solver"; break;
+        case POISSON_METHOD_REDBLACK_SOR: factory = "create_redblack_gpu_solver"; break;
+        case POISSON_METHOD_CG: factory = "create_cg_gpu_solver"; break;
+        default: return NULL; /* SOR / Gauss-Seidel / BiCGSTAB / multigrid: no GPU form */
+    }
+    poisson_solver_t* (*fn)(void) = (poisson_solver_t * (*)(void)) dlsym(RTLD_DEFAULT, factory);
+    if (!fn) {
+        cfd_set_error(CFD_ERROR_UNSUPPORTED, "libcfd_hip.so (GPU Poisson backend) is not loaded");
+        return NULL;
+    }
+    return fn();
+}
+
+cfd_status_t poisson_solver_init(poisson_solver_t* solver, size_t nx, size_t ny, size_t nz,
+                                 double dx, double dy, double dz,
+                                 const poisson_solver_params_t* params) {
+    /* linear_solver.c:237-282 */
+    if (!solver) return CFD_ERROR_INVALID;
+    if (nx < 3 || ny < 3 || (nz > 1 && nz < 3)) return CFD_ERROR_INVALID;
+    solver->nx = nx;
+    solver->ny = ny;
+    solver->nz = nz;
+    solver->dx = dx;
+    solver->dy = dy;
+    solver->dz = dz;
+    solver->params = params ? *params : poisson_solver_params_default();
+    if (solver->method == POISSON_METHOD_JACOBI && params == NULL)
+        solver->params.max_iterations = 2000;
+    if (solver->init) return solver->init(solver, nx, ny, nz, dx, dy, dz, &solver->params);
+    return CFD_SUCCESS;
+}
+
+void poisson_solver_destroy(poisson_solver_t* solver) {
+    /* linear_solver.c:284-294 */
+    if (!solver) return;
+    if (solver->destroy) solver->destroy(solver);
+    free(solver);
+}
+
+cfd_status_t poisson_solver_solve(poisson_solver_t* solver, double* x, double* x_temp,
+                                  const double* rhs, poisson_solver_stats_t* stats) {
+    /* linear_solver.c:487-509 (every GPU solver has its own solve) */
+    if (!solver) return CFD_ERROR_INVALID;
+    if (!solver->solve) return CFD_ERROR_UNSUPPORTED;
+    double t0 = now_ms();
+    cfd_status_t st = solver->solve(solver, x, x_temp, rhs, stats);
+    if (stats) stats->elapsed_time_ms = now_ms() - t0;
+    return st;
+}
+
+cfd_status_t poisson_solver_iterate(poisson_solver_t* solver, double* x, double* x_temp,
+                                    const double* rhs, double* residual) {
+    /* linear_solver.c:511-527 */
+    if (!solver || !x || !rhs) return CFD_ERROR_INVALID;
+    if (!solver->iterate) return CFD_ERROR_UNSUPPORTED;
+    return solver->iterate(solver, x, x_temp, rhs, residual);
+}

@@ -133,6 +133,27 @@ CFD_HIP_EXPORT simulation_data* load_simulation_from_checkpoint(const char* path
 CFD_HIP_EXPORT cfd_status_t restore_simulation_checkpoint(simulation_data* sim,
                                                           const char* path);
 
+/* ---- Poisson solver interface (poisson_solver.h:132-375, linear_solver.c:25-535)
+ * Only POISSON_BACKEND_GPU solvers exist here (the CPU backends are the
+ * reference's own); AUTO selects GPU when a HIP device is visible. The
+ * factories live in libcfd_hip.so (create_*_gpu_solver) and are found at run
+ * time, like the projection plugins. */
+CFD_HIP_EXPORT poisson_solver_params_t poisson_solver_params_default(void);
+CFD_HIP_EXPORT poisson_solver_stats_t poisson_solver_stats_default(void);
+CFD_HIP_EXPORT bool poisson_solver_backend_available(poisson_solver_backend_t backend);
+CFD_HIP_EXPORT poisson_solver_t* poisson_solver_create(poisson_solver_method_t method,
+                                                       poisson_solver_backend_t backend);
+CFD_HIP_EXPORT cfd_status_t poisson_solver_init(poisson_solver_t* solver, size_t nx, size_t ny,
+                                                size_t nz, double dx, double dy, double dz,
+                                                const poisson_solver_params_t* params);
+CFD_HIP_EXPORT void poisson_solver_destroy(poisson_solver_t* solver);
+CFD_HIP_EXPORT cfd_status_t poisson_solver_solve(poisson_solver_t* solver, double* x,
+                                                 double* x_temp, const double* rhs,
+                                                 poisson_solver_stats_t* stats);
+CFD_HIP_EXPORT cfd_status_t poisson_solver_iterate(poisson_solver_t* solver, double* x,
+                                                   double* x_temp, const double* rhs,
+                                                   double* residual);
+
 #ifdef __cplusplus
 }
 #endif

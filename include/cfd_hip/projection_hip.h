@@ -65,6 +65,14 @@ typedef struct {
     int sweep_variant;            /* CG sweep memory hints: bit0 non-temporal stores,
                                      bit1 non-temporal loads of single-use inputs, bit2 loads
                                      issued one plane ahead (built: 0-3, 4, 7; default 7) */
+    int rhs_density;              /* 1: rhs = (rho/dt) div u* (solver_projection.c:195-211,
+                                     default); 0: div u* / dt, the reference GPU's
+                                     (solver_projection_gpu.cu:706-707) */
+    int poisson_fail_fatal;       /* 1: a pressure solve that stops unconverged fails the
+                                     step with CFD_ERROR_MAX_ITER, field untouched
+                                     (solver_projection.c:220-224, default); 0: the step
+                                     continues with the capped solve, as the reference GPU
+                                     does (solver_projection_gpu.cu:717-733) */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
@@ -279,6 +287,13 @@ CFD_HIP_EXPORT ns_solver_t* create_projection_hip_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_rbsor_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_jacobi_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_rk4_hip_solver(void);
+/* poisson_solver_t GPU backend factories under the reference's names
+ * (linear_solver_internal.h:54-57; reached via poisson_solver_create(method,
+ * POISSON_BACKEND_GPU), linear_solver.c:150-235). Host-buffer semantics:
+ * solve uploads x and rhs, iterates in HBM, downloads x. */
+CFD_HIP_EXPORT poisson_solver_t* create_cg_gpu_solver(void);
+CFD_HIP_EXPORT poisson_solver_t* create_redblack_gpu_solver(void);
+CFD_HIP_EXPORT poisson_solver_t* create_jacobi_gpu_solver(void);
 /* Registers the four names above through cfd_registry_register(). */
 CFD_HIP_EXPORT void cfd_hip_register_solvers(ns_solver_registry_t* registry);
 

@@ -1139,3 +1139,96 @@ cfd_status_t oracle_rk4_step(flow_field* field, const grid* grid, const ns_solve
     }
     return CFD_SUCCESS;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Explicit pressure-relaxation step of the reference device API             */
+/* gpu_solver_step (lib/src/solvers/gpu/solver_projection_gpu.cu:523-570):   */
+/* kernel_velocity_rhs (:158-205) with inv_rho 1, kernel_velocity_update     */
+/* (:207-228), Neumann BC on u,v,w, kernel_compute_divergence (:78-95),      */
+/* kernel_pressure_update (:257-269), Neumann BC on p. The reference's        */
+/* device BC kernel writes all faces in one launch (its edge cells race);     */
+/* the restatement uses the sequential face order of                           */
+/* boundary_conditions_core_impl.h:41-85, which every race-free order of     */
+/* Neumann copies reproduces.                                                 */
+/* ------------------------------------------------------------------------ */
+cfd_status_t oracle_gpu_explicit_step(flow_field* f, const grid* g,
+                                      const ns_solver_params_t* prm) {
+    if (!f || !g || !prm) return CFD_ERROR_INVALID;
+    const size_t nx = f->nx, ny = f->ny, nz = f->nz, n = nx * ny * nz;
+    const size_t sz = (nz > 1) ? nx * ny : 0;
+    const size_t k0 = (nz > 1) ? 1 : 0, k1 = (nz > 1) ? nz - 2 : 0; /* inclusive */
+    const double dx = g->dx[0], dy = g->dy[0], dt = prm->dt, nu = prm->mu;
+    const double inv_2dx = 0.5 / dx, inv_2dy = 0.5 / dy;
+    const double inv_dx2 = 1.0 / (dx * dx), inv_dy2 = 1.0 / (dy * dy);
+    const double inv_2dz = (nz > 1) ? 0.5 / g->dz[0] : 0.0;
+    const double inv_dz2 = (nz > 1) ? 1.0 / (g->dz[0] * g->dz[0]) : 0.0;
+    const double inv_rho = 1.0;
+    double* ur = (double*)calloc(n, sizeof(double));
+    double* vr = (double*)calloc(n, sizeof(double));
+    double* wr = (double*)calloc(n, sizeof(double));
+    double* dv = (double*)calloc(n, sizeof(double));
+    if (!ur || !vr || !wr || !dv) {
+        free(ur); free(vr); free(wr); free(dv);
+        return CFD_ERROR_NOMEM;
+    }
+    double *u = f->u, *v = f->v, *w = f->w, *p = f->p;
+    for (size_t k = k0; k <= k1; k++)
+        for (size_t j = 1; j < ny - 1; j++)
+            for (size_t i = 1; i < nx - 1; i++) {
+                size_t idx = k * sz + j * nx + i;
+                double u_c = u[idx], v_c = v[idx], w_c = w[idx];
+                double du_dx = (u[idx + 1] - u[idx - 1]) * inv_2dx;
+                double du_dy = (u[idx + nx] - u[idx - nx]) * inv_2dy;
+                double du_dz = (u[idx + sz] - u[idx - sz]) * inv_2dz;
+                double d2u = (u[idx + 1] - 2.0 * u_c + u[idx - 1]) * inv_dx2 +
+                             (u[idx + nx] - 2.0 * u_c + u[idx - nx]) * inv_dy2 +
+                             (u[idx + sz] - 2.0 * u_c + u[idx - sz]) * inv_dz2;
+                double dv_dx = (v[idx + 1] - v[idx - 1]) * inv_2dx;
+                double dv_dy = (v[idx + nx] - v[idx - nx]) * inv_2dy;
+                double dv_dz = (v[idx + sz] - v[idx - sz]) * inv_2dz;
+                double d2v = (v[idx + 1] - 2.0 * v_c + v[idx - 1]) * inv_dx2 +
+                             (v[idx + nx] - 2.0 * v_c + v[idx - nx]) * inv_dy2 +
+                             (v[idx + sz] - 2.0 * v_c + v[idx - sz]) * inv_dz2;
+                double dw_dx = (w[idx + 1] - w[idx - 1]) * inv_2dx;
+                double dw_dy = (w[idx + nx] - w[idx - nx]) * inv_2dy;
+                double dw_dz = (w[idx + sz] - w[idx - sz]) * inv_2dz;
+                double d2w = (w[idx + 1] - 2.0 * w_c + w[idx - 1]) * inv_dx2 +
+                             (w[idx + nx] - 2.0 * w_c + w[idx - nx]) * inv_dy2 +
+                             (w[idx + sz] - 2.0 * w_c + w[idx - sz]) * inv_dz2;
+                double dp_dx = (p[idx + 1] - p[idx - 1]) * inv_2dx;
+                double dp_dy = (p[idx + nx] - p[idx - nx]) * inv_2dy;
+                double dp_dz = (p[idx + sz] - p[idx - sz]) * inv_2dz;
+                ur[idx] = -(u_c * du_dx + v_c * du_dy + w_c * du_dz) + nu * d2u - inv_rho * dp_dx;
+                vr[idx] = -(u_c * dv_dx + v_c * dv_dy + w_c * dv_dz) + nu * d2v - inv_rho * dp_dy;
+                wr[idx] = -(u_c * dw_dx + v_c * dw_dy + w_c * dw_dz) + nu * d2w - inv_rho * dp_dz;
+            }
+    for (size_t k = k0; k <= k1; k++)
+        for (size_t j = 1; j < ny - 1; j++)
+            for (size_t i = 1; i < nx - 1; i++) {
+                size_t idx = k * sz + j * nx + i;
+                u[idx] = clampv(u[idx] + dt * ur[idx]);
+                v[idx] = clampv(v[idx] + dt * vr[idx]);
+                w[idx] = clampv(w[idx] + dt * wr[idx]);
+            }
+    oracle_bc_neumann_3d(u, nx, ny, nz);
+    oracle_bc_neumann_3d(v, nx, ny, nz);
+    oracle_bc_neumann_3d(w, nx, ny, nz);
+    for (size_t k = k0; k <= k1; k++)
+        for (size_t j = 1; j < ny - 1; j++)
+            for (size_t i = 1; i < nx - 1; i++) {
+                size_t idx = k * sz + j * nx + i;
+                dv[idx] = (u[idx + 1] - u[idx - 1]) * inv_2dx + (v[idx + nx] - v[idx - nx]) * inv_2dy +
+                          (w[idx + sz] - w[idx - sz]) * inv_2dz;
+            }
+    const double ndim = (nz > 1) ? 3.0 : 2.0;
+    const double p_relax = 0.1 * dt * (inv_dx2 + inv_dy2 + inv_dz2) / ndim;
+    for (size_t k = k0; k <= k1; k++)
+        for (size_t j = 1; j < ny - 1; j++)
+            for (size_t i = 1; i < nx - 1; i++) {
+                size_t idx = k * sz + j * nx + i;
+                p[idx] -= p_relax * dv[idx];
+            }
+    oracle_bc_neumann_3d(p, nx, ny, nz);
+    free(ur); free(vr); free(wr); free(dv);
+    return CFD_SUCCESS;
+}

@@ -114,6 +114,11 @@ cfd_status_t oracle_apply_thermal_bcs(flow_field* field, const ns_solver_params_
 cfd_status_t oracle_rk4_step(flow_field* field, const grid* g, const ns_solver_params_t* params,
                              ns_solver_stats_t* stats);
 
+/* gpu_solver_step (solver_projection_gpu.cu:523-570): the reference device
+ * API's explicit pressure-relaxation step (not the projection). */
+cfd_status_t oracle_gpu_explicit_step(flow_field* field, const grid* g,
+                                      const ns_solver_params_t* params);
+
 /* solver_registry.c:31-62 */
 void oracle_max_velocity_pressure(const flow_field* f, double* max_vel, double* max_p);
 double oracle_max_temperature(const flow_field* f);

@@ -74,6 +74,7 @@ def lib():
             P(A.SolverStats))
         sig("oracle_energy_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
             C.c_double, C.c_double)
+        sig("oracle_gpu_explicit_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams))
         _lib = L
     return _lib
 
@@ -149,6 +150,11 @@ def rk4_step(field, grid, params):
     st = A.SolverStats()
     s = lib().oracle_rk4_step(field.ptr, grid.ptr, C.byref(params), C.byref(st))
     return s, st
+
+
+def gpu_explicit_step(field, grid, params) -> int:
+    """gpu_solver_step's explicit pressure-relaxation step (solver_projection_gpu.cu:523-570)."""
+    return lib().oracle_gpu_explicit_step(field.ptr, grid.ptr, C.byref(params))
 
 
 def apply_thermal_bcs(field, params) -> int:
