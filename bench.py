@@ -34,7 +34,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # rocprofv3 PMC summary of this workload (tools/gpu_profile.sh + prof_summary.py):
 # 2*FETCH_SIZE + WRITE_SIZE per working launch of sweep A, the gfx950
 # correction of MI355X_MICROARCH.md "HBM [CDNA4]".
-TRAFFIC_JSON = ROOT / "profiles" / "r01c_traffic_cg_sweeps.json"
+# Newest first; the first file that holds the kernel being reported is used.
+TRAFFIC_JSONS = [ROOT / "profiles" / "r01e_traffic_cg_sweeps.json",
+                 ROOT / "profiles" / "r01c_traffic_cg_sweeps.json"]
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
 BYTES_SWEEP_B = 24.0    # even iterations: read p, r; write r
@@ -60,7 +62,7 @@ def parse():
                     help="CG iterations in the 1-thread CPU sample (0: skip it)")
     ap.add_argument("--kchunk", type=int, default=0)
     ap.add_argument("--sweep-rows", type=int, default=16)
-    ap.add_argument("--sweep-variant", type=int, default=7,
+    ap.add_argument("--sweep-variant", type=int, default=15,
                     help="CG sweep variant: bit0 NT stores, bit1 NT loads, bit2 plane prefetch "
                          "(built: 0-4, 7)")
     return ap.parse_args()
@@ -266,15 +268,16 @@ def main():
 def pmc_traffic(kname, cells):
     """HBM bytes per launch of kernel `kname` from the committed PMC summary,
     if it was recorded for this kernel variant and grid size (else None)."""
-    try:
-        d = json.loads(TRAFFIC_JSON.read_text())
-    except (OSError, ValueError):
-        return None, None
-    if d.get("cells_per_launch") != float(cells):
-        return None, None
-    for k, v in d.get("kernels", {}).items():
-        if k == kname and "hbm_bytes_per_launch" in v:
-            return round(v["hbm_bytes_per_launch"]), f"{TRAFFIC_JSON.name}: {k}"
+    for path in TRAFFIC_JSONS:
+        try:
+            d = json.loads(path.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("cells_per_launch") != float(cells):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k == kname and "hbm_bytes_per_launch" in v:
+                return round(v["hbm_bytes_per_launch"]), f"{path.name}: {k}"
     return None, None
 
 

@@ -478,6 +478,21 @@ __device__ __forceinline__ RowPair row_pair(const SGeo& g) {
 // bundle of plane k+1 is issued before plane k is processed, so one plane of
 // loads stays in flight across the LDS barrier and the arithmetic.
 constexpr int SW_PREFETCH = 4;
+// bit 3: the two x-edge cells of a row (lane 0's left, lane 63's right
+// neighbour) are fetched by ONE load instruction with per-lane addresses;
+// bit 4: the centre rows of the inner waves of a stencil field (rows no
+// neighbouring tile re-reads as its y halo) are loaded non-temporally.
+constexpr int SW_EDGE1 = 8;
+constexpr int SW_NT_INNER = 16;
+
+template <bool NT>
+__device__ __forceinline__ double2 ld2n(const double* p, long long i) {
+    if (NT) {
+        d2x w = __builtin_nontemporal_load(reinterpret_cast<const d2x*>(p + i));
+        return make_double2(w.x, w.y);
+    }
+    return *reinterpret_cast<const double2*>(p + i);
+}
 
 __device__ __forceinline__ double2 fma2p(double2 a, double beta, double2 b) {
     return make_double2(a.x + beta * b.x, a.y + beta * b.y);
@@ -505,9 +520,14 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
     const bool xok = c.i0 < g.nx;
     const bool eok_l = c.lane == 0 && c.i0 >= 1 && xok;
     const bool eok_r = c.lane == 63 && c.i0 + 2 < g.nx;
+    constexpr bool E1 = (FL & SW_EDGE1) != 0;
+    const bool eok = eok_l || eok_r;
+    const long long eoff = (c.lane == 0) ? -1 : 2;
+    const bool inner = (FL & SW_NT_INNER) && !halo;
     const double2 zero = make_double2(0.0, 0.0);
     // raw r / p_old of: the centre of plane k+1, the y-halo row of plane k+1,
-    // the x-edge cells of plane k (p is formed from them when used)
+    // the x-edge cells of plane k (p is formed from them when used; with
+    // SW_EDGE1 lane 0's left and lane 63's right cell share lr / lo)
     struct Bundle {
         double2 cr, co, hr, ho;
         double lr, lo, rr, ro;
@@ -516,15 +536,26 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
         const double2 zero = make_double2(0.0, 0.0);  // a value, not the captured object
         Bundle b;
         const long long ip = ix + g.sz;
-        b.cr = xok ? ld2(r, ip) : zero;
-        b.co = (xok && !FIRST) ? ld2(po, ip) : zero;
+        if (inner) {
+            b.cr = xok ? ld2n<true>(r, ip) : zero;
+            b.co = (xok && !FIRST) ? ld2n<true>(po, ip) : zero;
+        } else {
+            b.cr = xok ? ld2(r, ip) : zero;
+            b.co = (xok && !FIRST) ? ld2(po, ip) : zero;
+        }
         const bool h = xok && halo && k + 1 < c.ke;
         b.hr = h ? ld2(r, ip + hoff) : zero;
         b.ho = (h && !FIRST) ? ld2(po, ip + hoff) : zero;
-        b.lr = eok_l ? r[ix - 1] : 0.0;
-        b.lo = (eok_l && !FIRST) ? po[ix - 1] : 0.0;
-        b.rr = eok_r ? r[ix + 2] : 0.0;
-        b.ro = (eok_r && !FIRST) ? po[ix + 2] : 0.0;
+        if (E1) {
+            b.lr = eok ? r[ix + eoff] : 0.0;
+            b.lo = (eok && !FIRST) ? po[ix + eoff] : 0.0;
+            b.rr = b.ro = 0.0;
+        } else {
+            b.lr = eok_l ? r[ix - 1] : 0.0;
+            b.lo = (eok_l && !FIRST) ? po[ix - 1] : 0.0;
+            b.rr = eok_r ? r[ix + 2] : 0.0;
+            b.ro = (eok_r && !FIRST) ? po[ix + 2] : 0.0;
+        }
         return b;
     };
     auto form2 = [&](double2 a, double2 b) { return FIRST ? a : fma2p(a, beta, b); };
@@ -563,7 +594,7 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
         double left = __shfl_up(pc.y, 1, 64);
         double right = __shfl_down(pc.x, 1, 64);
         if (c.lane == 0) left = form1(cur.lr, cur.lo);
-        if (c.lane == 63) right = form1(cur.rr, cur.ro);
+        if (c.lane == 63) right = E1 ? form1(cur.lr, cur.lo) : form1(cur.rr, cur.ro);
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
         if (c.act) {
@@ -635,9 +666,13 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
     const bool xok = c.i0 < g.nx;
     const bool eok_l = c.lane == 0 && c.i0 >= 1 && xok;
     const bool eok_r = c.lane == 63 && c.i0 + 2 < g.nx;
+    constexpr bool E1 = (FL & SW_EDGE1) != 0;
+    const bool eok = eok_l || eok_r;
+    const long long eoff = (c.lane == 0) ? -1 : 2;
+    const bool inner = (FL & SW_NT_INNER) && !halo;
     const double2 zero = make_double2(0.0, 0.0);
     // p of the centre and y-halo row of plane k+1; r, x, p_{it-1} and the
-    // x-edge p of plane k
+    // x-edge p of plane k (SW_EDGE1: both edge cells in el)
     struct Bundle {
         double2 pp, hp, rr, xo, qo;
         double el, er;
@@ -646,13 +681,19 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
         const double2 zero = make_double2(0.0, 0.0);  // a value, not the captured object
         Bundle b;
         const long long ip = ix + g.sz;
-        b.pp = xok ? ld2(p, ip) : zero;
+        if (inner) b.pp = xok ? ld2n<true>(p, ip) : zero;
+        else b.pp = xok ? ld2(p, ip) : zero;
         b.hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
         b.rr = xok ? ld2v<FL>(r, ix) : zero;
         b.xo = (FOLD && xok) ? ld2v<FL>(x, ix) : zero;
         b.qo = (FOLD && xok) ? ld2v<FL>(pprev, ix) : zero;
-        b.el = eok_l ? p[ix - 1] : 0.0;
-        b.er = eok_r ? p[ix + 2] : 0.0;
+        if (E1) {
+            b.el = eok ? p[ix + eoff] : 0.0;
+            b.er = 0.0;
+        } else {
+            b.el = eok_l ? p[ix - 1] : 0.0;
+            b.er = eok_r ? p[ix + 2] : 0.0;
+        }
         return b;
     };
     double acc = 0.0;
@@ -679,7 +720,7 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
         double left = __shfl_up(pc.y, 1, 64);
         double right = __shfl_down(pc.x, 1, 64);
         if (c.lane == 0) left = cur.el;
-        if (c.lane == 63) right = cur.er;
+        if (c.lane == 63) right = E1 ? cur.el : cur.er;
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
         double2 rn;

@@ -64,6 +64,12 @@ static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double
         case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, it);
         case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it);
         case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it);
+        case 15: if constexpr (TY == 16) return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it);
+                 [[fallthrough]];
+        case 23: if constexpr (TY == 16) return launch_cgA_f<TY, 23>(c, first, L, r, po, pn, it);
+                 [[fallthrough]];
+        case 31: if constexpr (TY == 16) return launch_cgA_f<TY, 31>(c, first, L, r, po, pn, it);
+                 [[fallthrough]];
         default: return launch_cgA_f<TY, 0>(c, first, L, r, po, pn, it);
     }
 }
@@ -76,6 +82,12 @@ static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BA
         case 3: return launch_cgB_f<TY, 3>(c, sg, L, a, it);
         case 4: return launch_cgB_f<TY, 4>(c, sg, L, a, it);
         case 7: return launch_cgB_f<TY, 7>(c, sg, L, a, it);
+        case 15: if constexpr (TY == 16) return launch_cgB_f<TY, 15>(c, sg, L, a, it);
+                 [[fallthrough]];
+        case 23: if constexpr (TY == 16) return launch_cgB_f<TY, 23>(c, sg, L, a, it);
+                 [[fallthrough]];
+        case 31: if constexpr (TY == 16) return launch_cgB_f<TY, 31>(c, sg, L, a, it);
+                 [[fallthrough]];
         default: return launch_cgB_f<TY, 0>(c, sg, L, a, it);
     }
 }
@@ -404,7 +416,8 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.kchunk = 0;
     c.verbose = 0;
     c.sweep_rows = 16;   // tools/sweep_bench.py at 512^3: 16 rows + NT hints fastest
-    c.sweep_variant = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH;  // r01c sweep_bench at 512^3
+    // r01c / r01e sweep_bench at 512^3 (profiles/r01e_sweep_variants.jsonl)
+    c.sweep_variant = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH | SW_EDGE1;
     c.rhs_density = 1;
     c.poisson_fail_fatal = 1;
     return c;
@@ -482,8 +495,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     // row-pair CG sweeps: 128 x TY x kc tiles (kernels.hpp, k_cgA / k_cgB)
     c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
     {   // variants built: 0-3 (memory hints), 4 and 7 (+ plane prefetch)
-        const int v = c->cfg.sweep_variant & 7;
-        c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : v;
+        const int v = c->cfg.sweep_variant & 31;
+        if ((v & 24) && (v & 7) == 7 && c->sweep_ty == 16) c->sweep_variant = v;  // 15, 23, 31
+        else c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : (v & 3);
     }
     SGeo& sg = c->sgeo;
     sg.nx = g.nx;

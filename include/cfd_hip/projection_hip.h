@@ -64,7 +64,10 @@ typedef struct {
                                      (default 16) */
     int sweep_variant;            /* CG sweep memory hints: bit0 non-temporal stores,
                                      bit1 non-temporal loads of single-use inputs, bit2 loads
-                                     issued one plane ahead (built: 0-3, 4, 7; default 7) */
+                                     issued one plane ahead, bit3 both x-edge cells of a row
+                                     in one load instruction, bit4 non-temporal loads of
+                                     inner-wave centre rows (built: 0-3, 4, 7; with 16 rows
+                                     also 15, 23, 31; default 15) */
     int rhs_density;              /* 1: rhs = (rho/dt) div u* (solver_projection.c:195-211,
                                      default); 0: div u* / dt, the reference GPU's
                                      (solver_projection_gpu.cu:706-707) */

@@ -203,7 +203,7 @@ def test_cg_sweep_variants_bitwise_equal(hip_lib, rows):
     xo = np.zeros_like(rhs)
     oracle.cg_solve(xo, rhs, g.dx, g.dy, g.dz)
     outs = []
-    for v in (0, 3, 4, 7):
+    for v in (0, 3, 4, 7, 15, 23, 31):
         ctx = api.HipProjection(33, 33, 33, sweep_rows=rows, sweep_variant=v)
         xh = np.zeros_like(rhs)
         sh, sth = ctx.poisson_solve(A.HIP_POISSON_CG, xh, rhs, g.dx, g.dy, g.dz)
