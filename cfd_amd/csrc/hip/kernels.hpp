@@ -484,6 +484,12 @@ constexpr int SW_PREFETCH = 4;
 // neighbouring tile re-reads as its y halo) are loaded non-temporally.
 constexpr int SW_EDGE1 = 8;
 constexpr int SW_NT_INNER = 16;
+// (r01e: asking for 8 waves per SIMD, i.e. <= 64 VGPRs and two 1024-thread
+// workgroups per CU, spills and is slower; profiles/r01e_sweep_variants.jsonl)
+template <int FL>
+constexpr int sweep_min_waves() {
+    return (FL & SW_PREFETCH) ? 4 : 1;
+}
 
 template <bool NT>
 __device__ __forceinline__ double2 ld2n(const double* p, long long i) {
@@ -502,7 +508,7 @@ __device__ __forceinline__ double2 fma2p(double2 a, double beta, double2 b) {
 // to pnew; (p, A p) with A p in registers. x is not touched here: sweep B of
 // every odd iteration folds the last two alpha p terms into x.
 template <int TY, bool FIRST, bool DIST, int FL = 0>
-static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_cgA(
+static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     SGeo g, Lap L, const double* __restrict__ r, const double* __restrict__ po,
     double* __restrict__ pn, CgState* st, double* partials, unsigned* counter, int it,
     double* dsum, Mbox* mb) {
@@ -646,7 +652,7 @@ static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_
 // :379-380, axpy :85-96) in their order, so x is bitwise the reference's while it is read
 // and written every other iteration only (p_{it-1} is the other p buffer).
 template <int TY, bool DIST, int FL = 0, bool FOLD = false>
-static __global__ __launch_bounds__(64 * TY, (FL & SW_PREFETCH) ? 4 : 1) void k_cgB(
+static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     SGeo g, Lap L, const double* __restrict__ p, double* __restrict__ r,
     const double* __restrict__ pprev, double* __restrict__ x, CgState* st, double* partials,
     unsigned* counter, int it, double* dsum, Mbox* mb) {

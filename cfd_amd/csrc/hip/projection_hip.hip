@@ -495,8 +495,8 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     // row-pair CG sweeps: 128 x TY x kc tiles (kernels.hpp, k_cgA / k_cgB)
     c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
     {   // variants built: 0-3 (memory hints), 4 and 7 (+ plane prefetch)
-        const int v = c->cfg.sweep_variant & 31;
-        if ((v & 24) && (v & 7) == 7 && c->sweep_ty == 16) c->sweep_variant = v;  // 15, 23, 31
+        const int v = c->cfg.sweep_variant & 63;
+        if ((v == 15 || v == 23 || v == 31) && c->sweep_ty == 16) c->sweep_variant = v;
         else c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : (v & 3);
     }
     SGeo& sg = c->sgeo;
