@@ -39,8 +39,8 @@ TRAFFIC_JSONS = [ROOT / "profiles" / "r01e_traffic_cg_sweeps.json",
                  ROOT / "profiles" / "r01c_traffic_cg_sweeps.json"]
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
-BYTES_SWEEP_B = 24.0    # even iterations: read p, r; write r
-BYTES_SWEEP_BX = 48.0   # odd iterations: + read x, p_prev; write x (two alpha p folded)
+BYTES_SWEEP_B = 24.0    # non-fold iterations: read p, r; write r
+BYTES_SWEEP_BX = 64.0   # every 4th iteration: + read x, p_{it-3..it-1}; write x (4 alpha p folded)
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
 BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
 

@@ -77,7 +77,8 @@ struct hip_proj_ctx {
     // fields
     double *u = nullptr, *v = nullptr, *w = nullptr, *p = nullptr, *T = nullptr;
     double *us = nullptr, *vs = nullptr, *ws = nullptr, *pn = nullptr;
-    double *r = nullptr, *pa = nullptr, *pb = nullptr;
+    double *r = nullptr, *pa = nullptr, *pb = nullptr;  // r; CG search directions
+    double *pc4 = nullptr, *pd4 = nullptr;               // (ring of CG_XFOLD = 4: pa pb pc4 pd4)
     double *rhs = nullptr, *xt = nullptr;
     double* Tn = nullptr;  // energy equation output (swapped with T)
     double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated

@@ -58,10 +58,15 @@ struct Lap {
     double dx2_inv, dy2_inv, inv_dz2;  // linear_solver_cg.c:103-110
 };
 
+// x is updated every CG_XFOLD iterations: sweep B of iteration it with
+// it % CG_XFOLD == CG_XFOLD - 1 folds the CG_XFOLD pending alpha_j p_j into x;
+// the search directions live in a ring of CG_XFOLD buffers (p_j in [j % CG_XFOLD]).
+constexpr int CG_XFOLD = 4;
+
 // Device-resident CG state; written only by the finishing (last) workgroup.
 struct CgState {
     double rho;     // (r, r) of the current residual
-    double alpha[2];// alpha_j of iteration j at [j & 1] (the fold needs two)
+    double alpha[CG_XFOLD];  // alpha_j of iteration j at [j % CG_XFOLD]
     double beta;    // beta for the next sweep A
     double pAp;
     double res;     // current residual 2-norm
@@ -222,8 +227,7 @@ __device__ __forceinline__ void fin_setup(CgState* st, double tot, double rel_to
     st->res = res0;
     st->tol = tol;
     st->abs_tol = abs_tol;
-    st->alpha[0] = 0.0;
-    st->alpha[1] = 0.0;
+    for (int q = 0; q < CG_XFOLD; ++q) st->alpha[q] = 0.0;
     st->beta = 0.0;
     st->pAp = 0.0;
     st->iterations = 0;
@@ -248,13 +252,13 @@ __device__ __forceinline__ void fin_A(CgState* st, double tot, int it) {
         st->status = ST_STAGNATED;
         st->iterations = it + 1;
     } else {
-        st->alpha[it & 1] = st->rho / tot;
+        st->alpha[it % CG_XFOLD] = st->rho / tot;
         st->nalpha = it + 1;
     }
 }
 
 // after (r, r): convergence test, rho breakdown, beta (linear_solver_cg.c:416-445).
-// fold: this sweep B also folded alpha_{it-1} p_{it-1} + alpha_it p_it into x.
+// fold: this sweep B also folded alpha_j p_j, j = it-CG_XFOLD+1 .. it, into x.
 __device__ __forceinline__ void fin_B(CgState* st, double tot, int it, bool fold) {
     if (fold) st->xdone = it + 1;
     double res = sqrt(tot);
@@ -647,22 +651,37 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
 
 // Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
 // to sweep A's), rho_new = (r, r), convergence test and beta.
-// FOLD (odd it): x = (x + alpha_{it-1} p_{it-1}) + alpha_it p_it, the
-// reference's two per-iteration updates x += alpha p (linear_solver_cg.c
-// :379-380, axpy :85-96) in their order, so x is bitwise the reference's while it is read
-// and written every other iteration only (p_{it-1} is the other p buffer).
+// FOLD (it % 4 == 3): x = (((x + a_{it-3} p_{it-3}) + a_{it-2} p_{it-2})
+// + a_{it-1} p_{it-1}) + a_it p_it, the reference's per-iteration updates
+// x += alpha p (linear_solver_cg.c:379-380, axpy :85-96) in their order with
+// the partial sums in registers, so x is bitwise the reference's while it is
+// read and written every fourth iteration only (p_{it-3..it-1} are the other
+// buffers of the p ring).
+struct PRing {
+    const double* p[CG_XFOLD];  // p_j at [j % CG_XFOLD]
+};
+struct PPrev {
+    const double* q[CG_XFOLD - 1];  // p_{it-3}, p_{it-2}, p_{it-1}
+};
+
 template <int TY, bool DIST, int FL = 0, bool FOLD = false>
 static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     SGeo g, Lap L, const double* __restrict__ p, double* __restrict__ r,
-    const double* __restrict__ pprev, double* __restrict__ x, CgState* st, double* partials,
+    PPrev pv, double* __restrict__ x, CgState* st, double* partials,
     unsigned* counter, int it, double* dsum, Mbox* mb) {
     constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
-    const double acur = st->alpha[it & 1];
-    const double aprev = FOLD ? st->alpha[(it + 1) & 1] : 0.0;
+    const double acur = st->alpha[it % CG_XFOLD];
+    double aq[CG_XFOLD - 1];
+#pragma unroll
+    for (int q = 0; q < CG_XFOLD - 1; ++q)
+        aq[q] = FOLD ? st->alpha[(it + 1 + q) % CG_XFOLD] : 0.0;  // alpha_{it-3+q}
+    const double* __restrict__ q0 = pv.q[0];
+    const double* __restrict__ q1 = pv.q[1];
+    const double* __restrict__ q2 = pv.q[2];
     const double malpha = -acur;
     RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
@@ -677,10 +696,10 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     const long long eoff = (c.lane == 0) ? -1 : 2;
     const bool inner = (FL & SW_NT_INNER) && !halo;
     const double2 zero = make_double2(0.0, 0.0);
-    // p of the centre and y-halo row of plane k+1; r, x, p_{it-1} and the
-    // x-edge p of plane k (SW_EDGE1: both edge cells in el)
+    // p of the centre and y-halo row of plane k+1; r, x, p_{it-3..it-1} and
+    // the x-edge p of plane k (SW_EDGE1: both edge cells in el)
     struct Bundle {
-        double2 pp, hp, rr, xo, qo;
+        double2 pp, hp, rr, xo, qa, qb, qc;
         double el, er;
     };
     auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
@@ -692,7 +711,9 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         b.hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
         b.rr = xok ? ld2v<FL>(r, ix) : zero;
         b.xo = (FOLD && xok) ? ld2v<FL>(x, ix) : zero;
-        b.qo = (FOLD && xok) ? ld2v<FL>(pprev, ix) : zero;
+        b.qa = (FOLD && xok) ? ld2v<FL>(q0, ix) : zero;
+        b.qb = (FOLD && xok) ? ld2v<FL>(q1, ix) : zero;
+        b.qc = (FOLD && xok) ? ld2v<FL>(q2, ix) : zero;
         if (E1) {
             b.el = eok ? p[ix + eoff] : 0.0;
             b.er = 0.0;
@@ -735,8 +756,12 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         if (c.act) st2v<FL>(r, idx, rn);
         if (FOLD && c.act) {
             double2 xw;
-            xw.x = c.in0 ? (cur.xo.x + aprev * cur.qo.x) + acur * pc.x : cur.xo.x;
-            xw.y = c.in1 ? (cur.xo.y + aprev * cur.qo.y) + acur * pc.y : cur.xo.y;
+            xw.x = c.in0 ? (((cur.xo.x + aq[0] * cur.qa.x) + aq[1] * cur.qb.x) +
+                            aq[2] * cur.qc.x) + acur * pc.x
+                         : cur.xo.x;
+            xw.y = c.in1 ? (((cur.xo.y + aq[0] * cur.qa.y) + aq[1] * cur.qb.y) +
+                            aq[2] * cur.qc.y) + acur * pc.y
+                         : cur.xo.y;
             st2v<FL>(x, idx, xw);
         }
         if (c.in0) acc += rn.x * rn.x;
@@ -771,20 +796,23 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
 }
 
 // Apply the x += alpha_j p_j the sweeps have not folded yet (j in [xdone,
-// nalpha): at most one, an even j, since every odd sweep B folds two).
-static __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, const double* __restrict__ p0,
-                                                    const double* __restrict__ p1,
+// nalpha), at most CG_XFOLD - 1 of them), in order, partial sums in a register
+// (bitwise the reference's sequential updates).
+static __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, PRing pr,
                                                     double* __restrict__ x, const CgState* st) {
-    if (st->xdone >= st->nalpha) return;
-    const int j = st->xdone;
-    const double alpha = st->alpha[j & 1];
-    const double* p = (j & 1) ? p1 : p0;
+    const int j0 = st->xdone, j1 = st->nalpha;  // at most CG_XFOLD - 1 pending
+    if (j0 >= j1) return;
     const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         TileCoord c = tile_coord(g, t);
         if (!c.active) continue;
         long long idx = cidx(g, c.i, c.j, c.kb);
-        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) x[idx] += alpha * p[idx];
+        for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+            double v = x[idx];
+            for (int jj = j0; jj < j1; ++jj)
+                v += st->alpha[jj % CG_XFOLD] * pr.p[jj % CG_XFOLD][idx];
+            x[idx] = v;
+        }
     }
 }
 

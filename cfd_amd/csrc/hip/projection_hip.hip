@@ -19,12 +19,12 @@ static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const d
                           c->counter, it, c->dsum, mbox(c));
 }
 
-// Sweep B operands: p = p_it (stencil), r, and for the fold (odd it) p_{it-1}
-// and x.
+// Sweep B operands: p = p_it (stencil), r, and for the fold (it % 4 == 3)
+// p_{it-3..it-1} and x.
 struct BArgs {
     const double* p;
     double* r;
-    const double* pprev;
+    PPrev pv;
     double* x;
 };
 
@@ -32,7 +32,7 @@ template <int TY, bool DIST, int FL, bool FOLD>
 static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
     const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
     hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, FOLD>), dim3(nb), dim3(64 * TY), 0, c->stream,
-                          c->ta, c->tb, 0, sg, L, a.p, a.r, a.pprev, a.x, c->st, c->partials,
+                          c->ta, c->tb, 0, sg, L, a.p, a.r, a.pv, a.x, c->st, c->partials,
                           c->counter, it, c->dsum, mbox(c));
 }
 
@@ -48,7 +48,7 @@ static void launch_cgA_f(hip_proj_ctx* c, bool first, const Lap& L, const double
 
 template <int TY, int FL>
 static void launch_cgB_f(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
-    const bool fold = (it & 1) != 0;
+    const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
     if (dist(c)) fold ? launch_cgB_t<TY, true, FL, true>(c, sg, L, a, it)
                       : launch_cgB_t<TY, true, FL, false>(c, sg, L, a, it);
     else fold ? launch_cgB_t<TY, false, FL, true>(c, sg, L, a, it)
@@ -154,14 +154,17 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                               c->st, c->dsum + 1, rel_tol, abs_tol, max_iter, check_interval);
     }
     if (D) ST_TRY(halo(c, {c->r}));
-    double* P[2] = {c->pa, c->pb};
+    double* P[CG_XFOLD] = {c->pa, c->pb, c->pc4, c->pd4};
     // one CG iteration: sweep A (+ all-reduce of (p,Ap); on slabs A also
     // forms p on the halo planes), sweep B (+ all-reduce of (r,r), halo of r)
     auto iterate = [&](int it) -> cfd_status_t {
-        double* pnew = P[it & 1];
-        double* pold = P[(it + 1) & 1];
-        const BArgs ba{pnew, c->r, pold, x};
-        const int kb = (it & 1) ? HIP_KT_CG_SWEEP_BX : HIP_KT_CG_SWEEP_B;
+        double* pnew = P[it % CG_XFOLD];
+        double* pold = P[(it + CG_XFOLD - 1) % CG_XFOLD];
+        const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
+        PPrev pv;
+        for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];  // p_{it-3+q}
+        const BArgs ba{pnew, c->r, pv, x};
+        const int kb = fold ? HIP_KT_CG_SWEEP_BX : HIP_KT_CG_SWEEP_B;
         timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, it); }, it);
         if (D && !mbox(c)) {
             ST_TRY(reduce_dot(c));
@@ -185,7 +188,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
             if (!mbox(c)) {
                 ST_TRY(reduce_dot(c));
                 hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
-                                      c->st, c->dsum + 1, it, it & 1);
+                                      c->st, c->dsum + 1, it, fold ? 1 : 0);
             }
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
         }
@@ -216,7 +219,9 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         slot ^= 1;
         chunk = std::min(chunk * 2, chunk_max);
     }
-    hipExtLaunchKernelGGL(k_cg_finalize, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, P[0], P[1], x,
+    PRing pr;
+    for (int q = 0; q < CG_XFOLD; ++q) pr.p[q] = P[q];
+    hipExtLaunchKernelGGL(k_cg_finalize, dim3(G), dim3(NT), 0, c->stream, c->ta, c->tb, 0, c->geo, pr, x,
                        c->st);
     HIP_TRY(hipMemcpyAsync(&c->h_state[2], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
                            c->stream));
@@ -550,7 +555,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
 
     const size_t n = field_elems(c);
     double** fields[] = {&c->u, &c->v, &c->w, &c->p, &c->us, &c->vs, &c->ws, &c->pn,
-                         &c->r, &c->pa, &c->pb};
+                         &c->r, &c->pa, &c->pb, &c->pc4, &c->pd4};
     for (double** f : fields) {
         cfd_status_t s = dalloc(c, f, n);
         if (s != CFD_SUCCESS) return s;

@@ -176,11 +176,12 @@ def test_poisson_cg_vs_oracle(hip_lib, n, expected):
     ctx.close()
 
 
-@pytest.mark.parametrize("iters", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("iters", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_poisson_cg_fixed_iterations_vs_oracle(hip_lib, iters):
-    """CG stopped by max_iterations after an odd or even count: sweep B folds
-    x every other iteration and the finalize kernel applies the last unfolded
-    alpha p, so x must hold exactly `iters` updates (linear_solver_cg.c:379-380)."""
+    """CG stopped by max_iterations after every residue of the fold period:
+    sweep B folds x every fourth iteration and the finalize kernel applies the
+    up to three unfolded alpha p, so x must hold exactly `iters` updates
+    (linear_solver_cg.c:379-380)."""
     g, rhs = cases.cos_rhs(17)
     prm = oracle.poisson_params(max_iterations=iters)
     xo = np.zeros_like(rhs)

@@ -2,7 +2,7 @@
 """CG sweep timing at n^3 for a list of context configurations.
 usage: sweep_bench.py "sweep_rows=8" "sweep_rows=16,kchunk=32" ...
 Each configuration runs 100 fixed CG iterations (no early exit) with
-dispatch-packet timing; prints per-sweep averages and GB/s (40 / 24 B/cell)."""
+dispatch-packet timing; prints per-sweep averages and GB/s (24 / 24 / 64 B/cell)."""
 import json
 import os
 import sys
@@ -42,7 +42,7 @@ def main():
                           "A_us": round(ua, 1), "B_us": round(ub, 1), "BX_us": round(ubx, 1),
                           "A_GBps": round(24 * cells / (ua * 1e-6) / 1e9, 1),
                           "B_GBps": round(24 * cells / (ub * 1e-6) / 1e9, 1),
-                          "BX_GBps": round(48 * cells / (ubx * 1e-6) / 1e9, 1)}), flush=True)
+                          "BX_GBps": round(64 * cells / (ubx * 1e-6) / 1e9, 1)}), flush=True)
 
 if __name__ == "__main__":
     main()
