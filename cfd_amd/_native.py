@@ -102,6 +102,14 @@ def _bind_host(lib) -> None:
     _sig(lib, "save_simulation_checkpoint", C.c_int, P(A.SimulationData), C.c_char_p)
     _sig(lib, "load_simulation_from_checkpoint", P(A.SimulationData), C.c_char_p)
     _sig(lib, "restore_simulation_checkpoint", C.c_int, P(A.SimulationData), C.c_char_p)
+    _sig(lib, "write_vtk_output", None, C.c_char_p, C.c_char_p, A.c_double_p, C.c_size_t,
+         C.c_size_t, C.c_size_t, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+         C.c_double)
+    _sig(lib, "write_vtk_vector_output", None, C.c_char_p, C.c_char_p, A.c_double_p,
+         A.c_double_p, A.c_double_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double, C.c_double,
+         C.c_double, C.c_double, C.c_double, C.c_double)
+    _sig(lib, "write_vtk_flow_field", None, C.c_char_p, P(A.FlowField), C.c_size_t, C.c_size_t,
+         C.c_size_t, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double)
     _sig(lib, "poisson_solver_params_default", A.PoissonParams)
     _sig(lib, "poisson_solver_stats_default", A.PoissonStats)
     _sig(lib, "poisson_solver_backend_available", C.c_bool, C.c_int)
@@ -175,6 +183,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "create_projection_hip_solver", P(A.NSSolver))
     _sig(lib, "create_rk4_hip_solver", P(A.NSSolver))
     _sig(lib, "cfd_hip_register_solvers", None, V)
+    _sig(lib, "hip_proj_write_vtk", C.c_int, V, C.c_char_p, P(A.Grid), C.c_double)
     _sig(lib, "create_cg_gpu_solver", P(A.PoissonSolver))
     _sig(lib, "create_redblack_gpu_solver", P(A.PoissonSolver))
     _sig(lib, "create_jacobi_gpu_solver", P(A.PoissonSolver))

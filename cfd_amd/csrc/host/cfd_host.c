@@ -9,6 +9,7 @@
  */
 #define _GNU_SOURCE
 #include "cfd_hip/cfd_host.h"
+#include "vtk_format.h"
 
 #include <dlfcn.h>
 #include <math.h>
@@ -680,4 +681,53 @@ cfd_status_t poisson_solver_iterate(poisson_solver_t* solver, double* x, double*
     if (!solver || !x || !rhs) return CFD_ERROR_INVALID;
     if (!solver->iterate) return CFD_ERROR_UNSUPPORTED;
     return solver->iterate(solver, x, x_temp, rhs, residual);
+}
+
+/* ------------------------------------------------------------------------ */
+/* legacy VTK output (vtk_output.c:110-275)                                  */
+/* ------------------------------------------------------------------------ */
+void write_vtk_output(const char* filename, const char* field_name, const double* data, size_t nx,
+                      size_t ny, size_t nz, double xmin, double xmax, double ymin, double ymax,
+                      double zmin, double zmax) {
+    if (!filename || !field_name || !data ||
+        !vtk_grid_ok(nx, ny, nz, xmin, xmax, ymin, ymax, zmin, zmax))
+        return;
+    FILE* fp = fopen(filename, "w");
+    if (!fp) {
+        cfd_set_error(CFD_ERROR_IO, "Failed to open VTK output file");
+        return;
+    }
+    vtk_header(fp, "CFD Framework Output", nx, ny, nz, xmin, xmax, ymin, ymax, zmin, zmax);
+    fprintf(fp, "\nPOINT_DATA %zu\n", nx * ny * nz);
+    vtk_scalars(fp, field_name, data, nx * ny * nz);
+    fclose(fp);
+}
+
+void write_vtk_vector_output(const char* filename, const char* field_name, const double* u_data,
+                             const double* v_data, const double* w_data, size_t nx, size_t ny,
+                             size_t nz, double xmin, double xmax, double ymin, double ymax,
+                             double zmin, double zmax) {
+    if (!filename || !field_name || !u_data || !v_data ||
+        !vtk_grid_ok(nx, ny, nz, xmin, xmax, ymin, ymax, zmin, zmax))
+        return;
+    FILE* fp = fopen(filename, "w");
+    if (!fp) {
+        cfd_set_error(CFD_ERROR_IO, "Failed to open VTK vector output file");
+        return;
+    }
+    vtk_header(fp, "CFD Framework Vector Output", nx, ny, nz, xmin, xmax, ymin, ymax, zmin, zmax);
+    fprintf(fp, "\nPOINT_DATA %zu\n", nx * ny * nz);
+    vtk_vectors(fp, field_name, u_data, v_data, w_data, nx * ny * nz);
+    fclose(fp);
+}
+
+void write_vtk_flow_field(const char* filename, const flow_field* field, size_t nx, size_t ny,
+                          size_t nz, double xmin, double xmax, double ymin, double ymax,
+                          double zmin, double zmax) {
+    if (!filename || !field || !vtk_grid_ok(nx, ny, nz, xmin, xmax, ymin, ymax, zmin, zmax))
+        return;
+    if (vtk_write_flow_field_file(filename, field->u, field->v, field->w, field->p, field->rho,
+                                  field->T, nx, ny, nz, xmin, xmax, ymin, ymax, zmin,
+                                  zmax) != 0)
+        cfd_set_error(CFD_ERROR_IO, "Failed to open VTK flow field output file");
 }

@@ -133,6 +133,22 @@ CFD_HIP_EXPORT simulation_data* load_simulation_from_checkpoint(const char* path
 CFD_HIP_EXPORT cfd_status_t restore_simulation_checkpoint(simulation_data* sim,
                                                           const char* path);
 
+/* ---- legacy VTK output (vtk_output.c:110-275): ASCII STRUCTURED_POINTS,
+ * same text as the reference writers. */
+CFD_HIP_EXPORT void write_vtk_output(const char* filename, const char* field_name,
+                                     const double* data, size_t nx, size_t ny, size_t nz,
+                                     double xmin, double xmax, double ymin, double ymax,
+                                     double zmin, double zmax);
+CFD_HIP_EXPORT void write_vtk_vector_output(const char* filename, const char* field_name,
+                                            const double* u_data, const double* v_data,
+                                            const double* w_data, size_t nx, size_t ny, size_t nz,
+                                            double xmin, double xmax, double ymin, double ymax,
+                                            double zmin, double zmax);
+CFD_HIP_EXPORT void write_vtk_flow_field(const char* filename, const flow_field* field,
+                                         size_t nx, size_t ny, size_t nz, double xmin,
+                                         double xmax, double ymin, double ymax, double zmin,
+                                         double zmax);
+
 /* ---- Poisson solver interface (poisson_solver.h:132-375, linear_solver.c:25-535)
  * Only POISSON_BACKEND_GPU solvers exist here (the CPU backends are the
  * reference's own); AUTO selects GPU when a HIP device is visible. The

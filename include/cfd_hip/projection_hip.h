@@ -212,6 +212,12 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_field_crc32(hip_proj_ctx_t* ctx, int field_
 CFD_HIP_EXPORT cfd_status_t cfd_hip_stream_bench(int device, size_t n, int reps,
                                                  double* copy_gbps, double* triad_gbps);
 
+/* VTK output of the resident state (vtk_output.c:196-275, write_vtk_flow_field
+ * text): velocity, pressure, density (the resident per-cell rho, else rho0),
+ * temperature (the resident T, else 0). Single-device contexts; g must match. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_write_vtk(hip_proj_ctx_t* ctx, const char* filename,
+                                               const grid* g, double rho0);
+
 /* Standalone pressure-Poisson solve on host buffers, the HIP counterpart of
  * poisson_solver_solve with a POISSON_BACKEND_GPU solver (linear_solver.c:487-509,
  * poisson_solver_cg_gpu.cu:135-178): upload x and rhs, solve lap(x) = rhs with
