@@ -51,13 +51,16 @@ def test_bench_one_gpu_contract(hip_lib):
     assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
 
 
-@pytest.mark.parametrize("case,world", [("cavity", 2), ("tg", 2), ("cavity", 4)])
-def test_bench_multi_rank_rehearsal(hip_lib, case, world):
+@pytest.mark.parametrize("case,world,size", [("cavity", 2, 66), ("tg", 2, 66), ("cavity", 4, 66),
+                                             ("cavity", 8, 130)])
+def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
+    """N ranks over RCCL on the one device; 8 ranks is the driver's largest
+    launch (here 128 interior planes = 16 per rank)."""
     env = _env()
     env["CFD_BENCH_SHARED_GPU"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", str(world),
-           "--size", "66", "--steps", "2", "--warmup", "1", "--case", case]
+           "--size", str(size), "--steps", "2", "--warmup", "1", "--case", case]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     d = _last_json(r.stdout)
