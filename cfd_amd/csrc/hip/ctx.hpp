@@ -88,6 +88,7 @@ struct hip_proj_ctx {
     std::vector<double> h_src_u, h_src_v;
     // reductions / state
     CgState* st = nullptr;
+    RxState* rxst = nullptr;             // fused relaxation loop state
     double* partials = nullptr;
     unsigned* counter = nullptr;
     unsigned long long* red = nullptr;   // [0] max vel, [1] max |p|, [2] nonfinite, [3] max T, [4] residual

@@ -838,33 +838,47 @@ __device__ __forceinline__ int bc_map(int c, int n, int mode) {
 // In a Z-slab the z faces exist only on the edge ranks (lo_face / hi_face);
 // the x/y ring is applied on every local plane, halo planes included (their
 // owner applies the identical gather to the same values).
-static __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f, int mode,
-                                                  DirVals dv) {
+// Boundary-shell cell e of the enumeration k_bc_shell / k_rx_shell share:
+// the x/y ring of every local plane, then the z faces the rank owns.
+__device__ __forceinline__ long long shell_total(const Geo& g) {
+    const bool is3d = g.nz > 1;
+    const long long ring = 2LL * g.nx + 2LL * (g.ny - 2);
+    const long long plane = (long long)g.nx * g.ny;
+    return ring * g.nz + ((is3d && g.lo_face) ? plane : 0) + ((is3d && g.hi_face) ? plane : 0);
+}
+__device__ __forceinline__ void shell_cell(const Geo& g, long long e, int& i, int& j, int& k,
+                                           bool& zlo, bool& zhi) {
     const bool is3d = g.nz > 1;
     const bool lo = is3d && g.lo_face, hi = is3d && g.hi_face;
     const long long ring = 2LL * g.nx + 2LL * (g.ny - 2);  // x/y boundary ring of one plane
     const long long nring = ring * g.nz;
     const long long plane = (long long)g.nx * g.ny;
-    const long long nzf = (lo ? plane : 0) + (hi ? plane : 0);
-    const long long total = nring + nzf;
+    if (e < nring) {
+        k = (int)(e / ring);
+        long long q = e % ring;
+        if (q < g.nx) { i = (int)q; j = 0; }
+        else if (q < 2LL * g.nx) { i = (int)(q - g.nx); j = g.ny - 1; }
+        else if (q < 2LL * g.nx + (g.ny - 2)) { i = 0; j = (int)(q - 2LL * g.nx) + 1; }
+        else { i = g.nx - 1; j = (int)(q - 2LL * g.nx - (g.ny - 2)) + 1; }
+    } else {
+        long long q = e - nring;
+        k = (lo && q < plane) ? 0 : g.nz - 1;
+        q = q % plane;
+        j = (int)(q / g.nx);
+        i = (int)(q % g.nx);
+    }
+    zlo = lo && k == 0;
+    zhi = hi && k == g.nz - 1;
+}
+
+static __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restrict__ f, int mode,
+                                                  DirVals dv) {
+    const long long total = shell_total(g);
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (long long)gridDim.x * blockDim.x) {
         int i, j, k;
-        if (e < nring) {
-            k = (int)(e / ring);
-            long long q = e % ring;
-            if (q < g.nx) { i = (int)q; j = 0; }
-            else if (q < 2LL * g.nx) { i = (int)(q - g.nx); j = g.ny - 1; }
-            else if (q < 2LL * g.nx + (g.ny - 2)) { i = 0; j = (int)(q - 2LL * g.nx) + 1; }
-            else { i = g.nx - 1; j = (int)(q - 2LL * g.nx - (g.ny - 2)) + 1; }
-        } else {
-            long long q = e - nring;
-            k = (lo && q < plane) ? 0 : g.nz - 1;
-            q = q % plane;
-            j = (int)(q / g.nx);
-            i = (int)(q % g.nx);
-        }
-        const bool zlo = lo && k == 0, zhi = hi && k == g.nz - 1;
+        bool zlo, zhi;
+        shell_cell(g, e, i, j, k, zlo, zhi);
         const long long dst = cidx(g, i, j, k);
         if (mode == 2) {
             double v;
@@ -1414,6 +1428,249 @@ static __global__ __launch_bounds__(NT) void k_residual_linf(Geo g, ResCoef rc,
         double a = sh[0];
         for (int w = 1; w < NWAVE; ++w) a = fmax(a, sh[w]);
         atomicMax(out, ord_enc(a));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Relaxation iterations on the row-pair sweep tiling (single device), with
+// the common loop's convergence test (linear_solver.c:397-485) on the device.
+// Ping-pong buffers: iteration it reads X = buf[it & 1] (the iterate after
+// it - 1 iterations, BCs applied) and leaves buf[(it + 1) & 1].
+//   RB-SOR:  k_rx<RX_RED>   X -> Y: first-colour ((i+j+k) odd, the CPU
+//                           reference's "red", linear_solver_redblack.c:97-114)
+//                           cells SOR-updated, the other cells copied; and the
+//                           L-inf residual of X;
+//            k_rx_shell     boundary shell X -> Y (the sweeps read it);
+//            k_rx<RX_BLACK> Y in place: second-colour cells (:116-133);
+//            k_rx_shell     Neumann BC on Y (poisson_solver_apply_bc).
+//   Jacobi:  k_rx<RX_JACOBI> X -> Y (linear_solver_jacobi.c:92-109) + the
+//            residual of X; k_rx_shell Neumann on Y.
+// The residual of the iterate after iteration it - 1 is thus computed by the
+// first sweep of iteration it, which has to read X anyway (16 B/cell of the
+// reference's separate residual pass saved); when it shows convergence the
+// result is X, still intact in its buffer, and everything launched after it
+// returns at once (RxState.done). Per-cell arithmetic is the reference's, and
+// L-inf (a max) is order-independent, so iterates, residuals and iteration
+// counts are bitwise the reference's.
+// ---------------------------------------------------------------------------
+struct RxState {
+    double tol, abs_tol, rel_tol, res0, res;
+    int iterations, done, status, max_iter, check_interval, result;  // result: buffer index
+};
+
+constexpr int RX_RED = 0;
+constexpr int RX_BLACK = 1;
+constexpr int RX_JACOBI = 2;
+
+// m = L-inf residual of the iterate after it - 1 iterations (it = 0: x0)
+__device__ __forceinline__ void rx_finish(RxState* st, double m, int it) {
+    if (it == 0) {  // linear_solver.c:415-437
+        st->res0 = m;
+        st->res = m;
+        double tol = st->rel_tol * m;
+        if (tol < st->abs_tol) tol = st->abs_tol;
+        st->tol = tol;
+        if (m < st->abs_tol) {
+            st->done = 1;
+            st->status = ST_CONVERGED;
+            st->iterations = 0;
+            st->result = 0;
+        }
+        return;
+    }
+    const int prev = it - 1;  // :443-468, iteration prev just completed
+    if (prev % st->check_interval == 0) {
+        st->res = m;
+        if (m < st->tol || m < st->abs_tol) {
+            st->done = 1;
+            st->status = ST_CONVERGED;
+            st->iterations = it;  // iter + 1 at the break
+            st->result = it & 1;
+            return;
+        }
+    }
+    if (it >= st->max_iter) {  // loop ran out: iterations = iter + 1 = max_iter + 1 (:472)
+        st->done = 1;
+        st->status = ST_MAX_ITER;
+        st->iterations = st->max_iter + 1;
+        st->result = it & 1;
+    }
+}
+
+static __global__ void k_rx_init(RxState* st, double rel_tol, double abs_tol, int max_iter,
+                                 int check_interval) {
+    if (threadIdx.x == 0) {
+        st->tol = 0.0;
+        st->abs_tol = abs_tol;
+        st->rel_tol = rel_tol;
+        st->res0 = st->res = 0.0;
+        st->iterations = 0;
+        st->done = 0;
+        st->status = ST_MAX_ITER;
+        st->max_iter = max_iter;
+        st->check_interval = check_interval;
+        st->result = 0;
+    }
+}
+
+// Boundary shell of an iteration: mode 0 copies src -> dst, mode 1 applies
+// the Neumann gathers to dst.
+static __global__ __launch_bounds__(256) void k_rx_shell(Geo g, const RxState* st,
+                                                  const double* __restrict__ src,
+                                                  double* __restrict__ dst, int mode) {
+    if (st->done) return;
+    const long long total = shell_total(g);
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        int i, j, k;
+        bool zlo, zhi;
+        shell_cell(g, e, i, j, k, zlo, zhi);
+        const long long d = cidx(g, i, j, k);
+        if (mode == 0) {
+            dst[d] = src[d];
+        } else {
+            const int sk = (zlo || zhi) ? bc_map(k, g.nz, 0) : k;
+            dst[d] = dst[cidx(g, bc_map(i, g.nx, 0), bc_map(j, g.ny, 0), sk)];
+        }
+    }
+}
+
+template <int TY, int MODE, int FL>
+static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
+    SGeo g, RelaxCoef rc, const double* __restrict__ xin, double* __restrict__ xout,
+    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
+    constexpr bool PF = (FL & SW_PREFETCH) != 0;
+    constexpr bool RES = MODE != RX_BLACK;
+    __shared__ double2 rows[2][TY + 2][64];
+    __shared__ double sh[TY];
+    __shared__ int flag;
+    if (st->done) return;
+    // stencil field: X (red / Jacobi) or Y in place (black)
+    const double* xs = (MODE == RX_BLACK) ? xout : xin;
+    RowPair c = row_pair<TY>(g);
+    const bool halo = (c.w == 0) || (c.w == TY - 1);
+    const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
+    const int hslot = (c.w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - min(c.j, g.ny - 1)) * g.px;
+    const bool xok = c.i0 < g.nx;
+    const bool eok = (c.lane == 0 && c.i0 >= 1 && xok) || (c.lane == 63 && c.i0 + 2 < g.nx);
+    const long long eoff = (c.lane == 0) ? -1 : 2;
+    // parity (i+j+k) of the pair's first cell at plane k is (j + k) & 1 (i0
+    // even); the first colour pass updates odd cells, the second even ones
+    const int upd = (MODE == RX_RED) ? 1 : 0;
+    const double2 zero = make_double2(0.0, 0.0);
+    struct Bundle {
+        double2 pp, hp, rr;  // X centre / y-halo of plane k+1; rhs of plane k
+        double el;           // x-edge cell of plane k
+    };
+    auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
+        const double2 zero = make_double2(0.0, 0.0);
+        Bundle b;
+        const long long ip = ix + g.sz;
+        b.pp = xok ? ld2(xs, ip) : zero;
+        b.hp = (xok && halo && k + 1 < c.ke) ? ld2(xs, ip + hoff) : zero;
+        b.rr = xok ? ld2v<FL>(rhs, ix) : zero;
+        b.el = eok ? xs[ix + eoff] : 0.0;
+        return b;
+    };
+    double m = 0.0;
+    long long idx = c.idx;
+    double2 pm = xok ? ld2(xs, idx - g.sz) : zero;
+    double2 pc = xok ? ld2(xs, idx) : zero;
+    double2 hc = (xok && halo) ? ld2(xs, idx + hoff) : zero;
+    Bundle cur;
+    if (PF) cur = issue(c.kb, idx);
+    int buf = 0;
+    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        Bundle nxt;
+        if (PF) {
+            if (k + 1 < c.ke) nxt = issue(k + 1, idx + g.ps);
+        } else {
+            cur = issue(k, idx);
+        }
+        rows[buf][c.w + 1][c.lane] = pc;
+        if (halo) rows[buf][hslot][c.lane] = hc;
+        __syncthreads();
+        const double2 ys = rows[buf][c.w][c.lane];
+        const double2 yn = rows[buf][c.w + 2][c.lane];
+        const double2 pp = cur.pp;
+        double left = __shfl_up(pc.y, 1, 64);
+        double right = __shfl_down(pc.x, 1, 64);
+        if (c.lane == 0) left = cur.el;
+        if (c.lane == 63) right = cur.el;
+        // cell 0: (xm, xp) = (left, pc.y); cell 1: (pc.x, right)
+        if (RES) {  // linear_solver.c:304-346 (k_residual_linf's expression)
+            const double l0 = (pc.y - 2.0 * pc.x + left) / rc.dx2 +
+                              (yn.x - 2.0 * pc.x + ys.x) / rc.dy2 +
+                              (pp.x + pm.x - 2.0 * pc.x) * rc.inv_dz2;
+            const double l1 = (right - 2.0 * pc.y + pc.x) / rc.dx2 +
+                              (yn.y - 2.0 * pc.y + ys.y) / rc.dy2 +
+                              (pp.y + pm.y - 2.0 * pc.y) * rc.inv_dz2;
+            const double r0 = fabs(l0 - cur.rr.x), r1 = fabs(l1 - cur.rr.y);
+            if (c.in0 && r0 > m) m = r0;
+            if (c.in1 && r1 > m) m = r1;
+        }
+        double2 out = pc;
+        if (MODE == RX_JACOBI) {
+            const double pn0 = -(cur.rr.x - (pc.y + left) / rc.dx2 - (yn.x + ys.x) / rc.dy2 -
+                                 (pp.x + pm.x) * rc.inv_dz2) *
+                               rc.inv_factor;
+            const double pn1 = -(cur.rr.y - (right + pc.x) / rc.dx2 - (yn.y + ys.y) / rc.dy2 -
+                                 (pp.y + pm.y) * rc.inv_dz2) *
+                               rc.inv_factor;
+            if (c.in0) out.x = pn0;
+            if (c.in1) out.y = pn1;
+        } else {
+            // one cell of the pair has this pass's colour: gather its stencil
+            // (wave-uniform choice: the parity depends on j and k only)
+            const bool first = ((c.j + k) & 1) == upd;  // single device: local = global index
+            const double xc = first ? pc.x : pc.y;
+            const double xl = first ? left : pc.x, xr = first ? pc.y : right;
+            const double yl = first ? ys.x : ys.y, yr = first ? yn.x : yn.y;
+            const double zl = first ? pm.x : pm.y, zr = first ? pp.x : pp.y;
+            const double rh = first ? cur.rr.x : cur.rr.y;
+            const double pn = -(rh - (xr + xl) / rc.dx2 - (yr + yl) / rc.dy2 - (zr + zl) * rc.inv_dz2) *
+                              rc.inv_factor;
+            const double xn = xc + rc.omega * (pn - xc);
+            if (first) {
+                if (c.in0) out.x = xn;
+            } else if (c.in1) {
+                out.y = xn;
+            }
+        }
+        if (c.act) st2v<FL>(xout, idx, out);
+        pm = pc;
+        pc = pp;
+        hc = cur.hp;
+        if (PF) cur = nxt;
+        buf ^= 1;
+    }
+    if (!RES) return;
+    m = wave_max(m);
+    if (c.lane == 0) sh[c.w] = m;
+    __syncthreads();
+    double* shs = (double*)&rows[0][0][0];
+    if (threadIdx.x == 0) {
+        double a = 0.0;
+        for (int q = 0; q < TY; ++q) a = fmax(a, sh[q]);
+        store_sc1(&partials[blockIdx.x], a);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        flag = (t == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (flag == 0) return;
+    double a = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 64 * TY) a = fmax(a, load_sc1(&partials[b]));
+    a = wave_max(a);
+    if (c.lane == 0) shs[c.w] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = 0.0;
+        for (int q = 0; q < TY; ++q) tot = fmax(tot, shs[q]);
+        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rx_finish(st, tot, it);
     }
 }
 

@@ -275,6 +275,85 @@ static cfd_status_t residual_linf(hip_proj_ctx* c, const double* x, const ResCoe
     return CFD_SUCCESS;
 }
 
+static cfd_status_t ensure_aux(hip_proj_ctx* c, bool need_rhs, bool need_xt);
+static_assert(sizeof(RxState) <= sizeof(CgState), "RxState polls through the CgState slots");
+
+// Fused relaxation loop (single device, 16-row sweep tiles): the iteration's
+// sweeps, boundary shell and convergence test all run on the device (k_rx,
+// kernels.hpp); the host polls the state one chunk behind, like cg_solve.
+// Same iterates, residuals, iteration counts and statuses as relax_solve's
+// two-pass form below.
+static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCoef& rc,
+                                      double rel_tol, double abs_tol, int max_iter,
+                                      int check_interval) {
+    ST_TRY(ensure_aux(c, true, true));
+    if (!c->rxst) HIP_TRY(hipMalloc((void**)&c->rxst, sizeof(RxState)));
+    double* X[2] = {c->pn, c->xt};
+    const unsigned nb = (unsigned)sweep_grid(c);
+    constexpr int FL = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH | SW_EDGE1;
+    hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
+                          rel_tol, abs_tol, max_iter, check_interval);
+    auto iterate = [&](int it) {
+        double* xi = X[it & 1];
+        double* xo = X[(it + 1) & 1];
+        if (method == HIP_POISSON_REDBLACK) {
+            timed(c, HIP_KT_RELAX, [&] {
+                hipExtLaunchKernelGGL((k_rx<16, RX_RED, FL>), dim3(nb), dim3(1024), 0, c->stream,
+                                      c->ta, c->tb, 0, c->sgeo, rc, xi, xo, c->rhs, c->rxst,
+                                      c->partials, c->counter, it);
+            });
+            hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream,
+                                  c->ta, c->tb, 0, c->geo, c->rxst, xi, xo, 0);
+            timed(c, HIP_KT_RELAX, [&] {
+                hipExtLaunchKernelGGL((k_rx<16, RX_BLACK, FL>), dim3(nb), dim3(1024), 0,
+                                      c->stream, c->ta, c->tb, 0, c->sgeo, rc, nullptr, xo,
+                                      c->rhs, c->rxst, c->partials, c->counter, it);
+            });
+        } else {
+            timed(c, HIP_KT_RELAX, [&] {
+                hipExtLaunchKernelGGL((k_rx<16, RX_JACOBI, FL>), dim3(nb), dim3(1024), 0,
+                                      c->stream, c->ta, c->tb, 0, c->sgeo, rc, xi, xo, c->rhs,
+                                      c->rxst, c->partials, c->counter, it);
+            });
+        }
+        hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
+                              c->tb, 0, c->geo, c->rxst, nullptr, xo, 1);
+    };
+    // iterations 0..max_iter: sweep it also yields the residual after it - 1
+    // iterations, so the last launch only completes the final test
+    RxState* hs = reinterpret_cast<RxState*>(c->h_state);  // pinned, >= 3 RxState
+    int it = 0, chunk = 8, slot = 0, prev = -1;
+    const int chunk_max = std::max(1, c->cfg.poll_interval);
+    while (it <= max_iter) {
+        const int n = std::min(chunk, max_iter + 1 - it);
+        for (int q = 0; q < n; ++q, ++it) iterate(it);
+        HIP_TRY(hipMemcpyAsync(&hs[slot], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
+        if (prev >= 0) {
+            HIP_TRY(hipEventSynchronize(c->ev_poll[prev]));
+            if (hs[prev].done) break;
+        }
+        prev = slot;
+        slot ^= 1;
+        chunk = std::min(chunk * 2, chunk_max);
+    }
+    HIP_TRY(hipMemcpyAsync(&hs[2], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    flush_timing(c);
+    const RxState& r = hs[2];
+    if (!r.done) {
+        set_err(CFD_ERROR, "relaxation: device loop ended without a decision");
+        return CFD_ERROR;
+    }
+    if (r.result == 1) std::swap(c->pn, c->xt);
+    c->pstats.initial_residual = r.res0;
+    c->pstats.iterations = r.iterations;
+    c->pstats.final_residual = r.res;
+    c->pstats.status = (poisson_solver_status_t)r.status;
+    return (r.status == ST_CONVERGED) ? CFD_SUCCESS : CFD_ERROR_MAX_ITER;
+}
+
 // Relaxation methods driven by the common loop (linear_solver.c:397-485):
 // L-infinity residual before the loop and every check_interval iterations.
 static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double dy, double dz,
@@ -287,6 +366,8 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     rc.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
     rc.inv_factor = 1.0 / (2.0 * (1.0 / rc.dx2 + 1.0 / rc.dy2 + rc.inv_dz2));
     rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nzg, dx, dy, dz) : omega_in;
+    if (!dist(c) && c->sweep_ty == 16 && max_iter > 0 && !c->cfg.relax_two_pass)
+        return relax_solve_fused(c, method, rc, rel_tol, abs_tol, max_iter, check_interval);
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
     const DirVals dv{};
     ST_TRY(halo(c, {c->pn}));
@@ -425,6 +506,7 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.sweep_variant = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH | SW_EDGE1;
     c.rhs_density = 1;
     c.poisson_fail_fatal = 1;
+    c.relax_two_pass = 0;
     return c;
 }
 
@@ -439,6 +521,7 @@ static void free_ctx(hip_proj_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void* b : c->allocs) hipFree(b);
     if (c->st) hipFree(c->st);
+    if (c->rxst) hipFree(c->rxst);
     if (c->partials) hipFree(c->partials);
     if (c->counter) hipFree(c->counter);
     if (c->red) hipFree(c->red);

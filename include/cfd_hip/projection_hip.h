@@ -76,6 +76,9 @@ typedef struct {
                                      (solver_projection.c:220-224, default); 0: the step
                                      continues with the capped solve, as the reference GPU
                                      does (solver_projection_gpu.cu:717-733) */
+    int relax_two_pass;           /* RB-SOR / Jacobi: 1 = separate colour passes + residual
+                                     pass with a host check per iteration (the r01 form);
+                                     0 = fused device loop (default, single device) */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;

@@ -235,6 +235,58 @@ def test_poisson_relax_bitwise(hip_lib, method):
     ctx.close()
 
 
+@pytest.mark.parametrize("method", [A.HIP_POISSON_REDBLACK, A.HIP_POISSON_JACOBI])
+@pytest.mark.parametrize("shape,kw", [
+    ((17, 17, 17), dict()),                                   # converges
+    ((23, 19, 14), dict(max_iterations=7)),                   # capped: iterations = 8
+    ((33, 29, 1), dict(check_interval=5)),                    # 2-D, sparse checks
+    ((130, 20, 9), dict(max_iterations=40, check_interval=3)),  # two x tiles, odd ny
+    ((17, 17, 17), dict(tolerance=1e-2)),                     # early stop, odd iterate
+])
+def test_poisson_relax_fused_loop_bitwise(hip_lib, method, shape, kw):
+    """The fused device loop (k_rx, lagged residual, ping-pong buffers) and
+    the two-pass form both equal the oracle bit for bit: iterate, iteration
+    count (max_iterations + 1 when capped, linear_solver.c:472), status,
+    initial and final residual."""
+    nx, ny, nz = shape
+    rng = np.random.default_rng(nx * 7 + nz)
+    rhs = rng.standard_normal((nz, ny, nx))
+    x0 = 0.1 * rng.standard_normal((nz, ny, nx))
+    d = 1.0 / (nx - 1)
+    dz = 1.0 / (nz - 1) if nz > 1 else 0.0
+    base = dict(max_iterations=3000 if method == A.HIP_POISSON_JACOBI else 2000)
+    base.update(kw)
+    prm = oracle.poisson_params(**base)
+    xo = x0.copy()
+    if method == A.HIP_POISSON_REDBLACK:
+        so, sto = oracle.redblack_solve(xo, rhs, d, d, dz, prm)
+    else:
+        so, sto = oracle.jacobi_solve(xo, rhs, d, d, dz, prm)
+    for two_pass in (0, 1):
+        ctx = api.HipProjection(nx, ny, nz, relax_two_pass=two_pass)
+        xh = x0.copy()
+        sh, sth = ctx.poisson_solve(method, xh, rhs, d, d, dz, prm)
+        ctx.close()
+        assert sh == so, two_pass
+        assert (sth.iterations, sth.status) == (sto.iterations, sto.status), two_pass
+        assert sth.initial_residual == sto.initial_residual
+        assert sth.final_residual == sto.final_residual
+        np.testing.assert_array_equal(xh, xo)
+
+
+def test_poisson_relax_initially_converged(hip_lib):
+    """linear_solver.c:429-437: residual below the absolute tolerance before
+    the loop -> 0 iterations, x untouched."""
+    g, rhs = cases.cos_rhs(17)
+    prm = oracle.poisson_params(absolute_tolerance=1e6)
+    ctx = api.HipProjection(17, 17, 17)
+    x = np.full_like(rhs, 0.25)
+    sh, sth = ctx.poisson_solve(A.HIP_POISSON_REDBLACK, x, rhs, g.dx, g.dy, g.dz, prm)
+    ctx.close()
+    assert sh == A.CFD_SUCCESS and sth.iterations == 0 and sth.status == A.POISSON_CONVERGED
+    assert np.all(x == 0.25)
+
+
 def test_deterministic(hip_lib):
     """Fixed-order reductions: two runs are bitwise identical."""
     g, f, p = cases.tg3(33)
