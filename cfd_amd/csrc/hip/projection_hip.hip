@@ -64,7 +64,7 @@ static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double
         case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, it);
         case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it);
         case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it);
-        case 15: if constexpr (TY == 16) return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it);
+        case 15: return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it);
                  [[fallthrough]];
         case 23: if constexpr (TY == 16) return launch_cgA_f<TY, 23>(c, first, L, r, po, pn, it);
                  [[fallthrough]];
@@ -82,7 +82,7 @@ static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BA
         case 3: return launch_cgB_f<TY, 3>(c, sg, L, a, it);
         case 4: return launch_cgB_f<TY, 4>(c, sg, L, a, it);
         case 7: return launch_cgB_f<TY, 7>(c, sg, L, a, it);
-        case 15: if constexpr (TY == 16) return launch_cgB_f<TY, 15>(c, sg, L, a, it);
+        case 15: return launch_cgB_f<TY, 15>(c, sg, L, a, it);
                  [[fallthrough]];
         case 23: if constexpr (TY == 16) return launch_cgB_f<TY, 23>(c, sg, L, a, it);
                  [[fallthrough]];
@@ -584,7 +584,8 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
     {   // variants built: 0-3 (memory hints), 4 and 7 (+ plane prefetch)
         const int v = c->cfg.sweep_variant & 63;
-        if ((v == 15 || v == 23 || v == 31) && c->sweep_ty == 16) c->sweep_variant = v;
+        if (v == 15 && c->sweep_ty >= 8) c->sweep_variant = v;
+        else if ((v == 23 || v == 31) && c->sweep_ty == 16) c->sweep_variant = v;
         else c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : (v & 3);
     }
     SGeo& sg = c->sgeo;
