@@ -400,6 +400,7 @@ struct SGeo {
     // (same stream, so the later launch) finishes the reduction.
     int kmode;
     int part_ofs, part_total;
+    int kofs;  // global index of local plane 0 (Z-slabs; colour parity)
 };
 
 __device__ __forceinline__ int xcd_tile(int b, int nt) {
@@ -1535,10 +1536,14 @@ static __global__ __launch_bounds__(256) void k_rx_shell(Geo g, const RxState* s
     }
 }
 
-template <int TY, int MODE, int FL>
+// Z-slabs (DIST): the residual is an all-ranks max, through the device
+// mailbox (mb) or, without one, left encoded in dred[0] for an RCCL max
+// all-reduce + k_rx_finish.
+template <int TY, int MODE, int FL, bool DIST = false>
 static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
     SGeo g, RelaxCoef rc, const double* __restrict__ xin, double* __restrict__ xout,
-    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
+    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
+    Mbox* mb, unsigned long long* dred) {
     constexpr bool PF = (FL & SW_PREFETCH) != 0;
     constexpr bool RES = MODE != RX_BLACK;
     __shared__ double2 rows[2][TY + 2][64];
@@ -1555,8 +1560,8 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
     const bool xok = c.i0 < g.nx;
     const bool eok = (c.lane == 0 && c.i0 >= 1 && xok) || (c.lane == 63 && c.i0 + 2 < g.nx);
     const long long eoff = (c.lane == 0) ? -1 : 2;
-    // parity (i+j+k) of the pair's first cell at plane k is (j + k) & 1 (i0
-    // even); the first colour pass updates odd cells, the second even ones
+    // parity (i+j+k) of the pair's first cell at local plane k is
+    // (j + k + kofs) & 1 (i0 even); the first colour pass updates odd cells
     const int upd = (MODE == RX_RED) ? 1 : 0;
     const double2 zero = make_double2(0.0, 0.0);
     struct Bundle {
@@ -1623,7 +1628,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
         } else {
             // one cell of the pair has this pass's colour: gather its stencil
             // (wave-uniform choice: the parity depends on j and k only)
-            const bool first = ((c.j + k) & 1) == upd;  // single device: local = global index
+            const bool first = ((c.j + k + g.kofs) & 1) == upd;  // global parity
             const double xc = first ? pc.x : pc.y;
             const double xl = first ? left : pc.x, xr = first ? pc.y : right;
             const double yl = first ? ys.x : ys.y, yr = first ? yn.x : yn.y;
@@ -1670,8 +1675,31 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
         double tot = 0.0;
         for (int q = 0; q < TY; ++q) tot = fmax(tot, shs[q]);
         __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rx_finish(st, tot, it);
+        if (!DIST) {
+            rx_finish(st, tot, it);
+        } else if (mb) {
+            double gm;
+            if (mbox_allreduce(mb, tot, &gm, true)) {
+                rx_finish(st, gm, it);
+            } else {
+                st->done = 1;
+                st->status = ST_COMM_TIMEOUT;
+            }
+        } else {
+            dred[0] = ord_enc(tot);
+        }
     }
+}
+
+__device__ __forceinline__ double ord_dec_dev(unsigned long long e) {
+    const unsigned long long b =
+        (e & 0x8000000000000000ull) ? (e & 0x7FFFFFFFFFFFFFFFull) : ~e;
+    return __longlong_as_double((long long)b);
+}
+
+// after the RCCL max all-reduce of dred (Z-slabs without a device mailbox)
+static __global__ void k_rx_finish(RxState* st, const unsigned long long* gred, int it) {
+    if (threadIdx.x == 0 && !st->done) rx_finish(st, ord_dec_dev(gred[0]), it);
 }
 
 }  // namespace cfdhip

@@ -22,10 +22,12 @@ struct Mbox {
 // rank holds the same bits. The sequence counter lives on the device and
 // advances only when a reduction actually runs, so consecutive reductions
 // alternate parity and a slot is never overwritten before its reader has
-// consumed it. A bounded wait (timeout_ticks of wall_clock64) turns a lost
+// consumed it. take_max: the maximum instead of the sum (L-inf residuals).
+// A bounded wait (timeout_ticks of wall_clock64) turns a lost
 // peer into a reported error instead of a hung GPU.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool mbox_allreduce(Mbox* mb, double v, double* out) {
+__device__ __forceinline__ bool mbox_allreduce(Mbox* mb, double v, double* out,
+                                               bool take_max = false) {
     const unsigned long long seq = mb->count + 1;
     mb->count = seq;
     const int n = mb->n, me = mb->rank;
@@ -45,8 +47,9 @@ __device__ __forceinline__ bool mbox_allreduce(Mbox* mb, double v, double* out) 
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > mb->timeout_ticks) return false;
         }
-        sum += __longlong_as_double(
+        const double x = __longlong_as_double(
             (long long)__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        sum = take_max ? (r == 0 ? x : fmax(sum, x)) : sum + x;
     }
     *out = sum;
     return true;

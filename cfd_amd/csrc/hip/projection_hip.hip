@@ -289,35 +289,65 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     ST_TRY(ensure_aux(c, true, true));
     if (!c->rxst) HIP_TRY(hipMalloc((void**)&c->rxst, sizeof(RxState)));
     double* X[2] = {c->pn, c->xt};
+    const bool D = dist(c);
+    Mbox* mb = mbox(c);
+    // Z-slabs without a device mailbox: residual max through RCCL (red[6] -> redg[6])
+    unsigned long long* dred = c->red + 6;
+    unsigned long long* gred = D ? c->redg + 6 : nullptr;
     const unsigned nb = (unsigned)sweep_grid(c);
+    const unsigned TH = 64u * (unsigned)c->sweep_ty;
     constexpr int FL = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH | SW_EDGE1;
+    auto sweep = [&](int mode, const double* xi, double* xo, int it) {
+        timed(c, HIP_KT_RELAX, [&] {
+#define RX_LAUNCH(TYV, M, DV)                                                                  \
+    hipExtLaunchKernelGGL((k_rx<TYV, M, FL, DV>), dim3(nb), dim3(TH), 0, c->stream, c->ta,     \
+                          c->tb, 0, c->sgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,        \
+                          c->counter, it, mb, dred)
+#define RX_MODES(TYV, DV)                                 \
+    if (mode == RX_RED) RX_LAUNCH(TYV, RX_RED, DV);       \
+    else if (mode == RX_BLACK) RX_LAUNCH(TYV, RX_BLACK, DV); \
+    else RX_LAUNCH(TYV, RX_JACOBI, DV)
+            if (c->sweep_ty == 16) {
+                if (D) { RX_MODES(16, true); } else { RX_MODES(16, false); }
+            } else {
+                if (D) { RX_MODES(8, true); } else { RX_MODES(8, false); }
+            }
+#undef RX_MODES
+#undef RX_LAUNCH
+        });
+    };
+    // the residual sweep's all-ranks max when there is no device mailbox
+    auto finish = [&](int it) -> cfd_status_t {
+        if (!D || mb) return CFD_SUCCESS;
+        ST_TRY(c->comm->allreduce_max_u64(c->stream, dred, gred, 1));
+        hipExtLaunchKernelGGL(k_rx_finish, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
+                              c->rxst, gred, it);
+        return CFD_SUCCESS;
+    };
+    ST_TRY(halo(c, {c->pn}));
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
                           rel_tol, abs_tol, max_iter, check_interval);
-    auto iterate = [&](int it) {
+    // Halo exchanges are host-launched and run even after the device decided
+    // to stop; they then copy the neighbours' final owned planes into the
+    // result's halo planes, which is what they hold anyway.
+    auto iterate = [&](int it) -> cfd_status_t {
         double* xi = X[it & 1];
         double* xo = X[(it + 1) & 1];
         if (method == HIP_POISSON_REDBLACK) {
-            timed(c, HIP_KT_RELAX, [&] {
-                hipExtLaunchKernelGGL((k_rx<16, RX_RED, FL>), dim3(nb), dim3(1024), 0, c->stream,
-                                      c->ta, c->tb, 0, c->sgeo, rc, xi, xo, c->rhs, c->rxst,
-                                      c->partials, c->counter, it);
-            });
+            sweep(RX_RED, xi, xo, it);
+            ST_TRY(finish(it));
             hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream,
                                   c->ta, c->tb, 0, c->geo, c->rxst, xi, xo, 0);
-            timed(c, HIP_KT_RELAX, [&] {
-                hipExtLaunchKernelGGL((k_rx<16, RX_BLACK, FL>), dim3(nb), dim3(1024), 0,
-                                      c->stream, c->ta, c->tb, 0, c->sgeo, rc, nullptr, xo,
-                                      c->rhs, c->rxst, c->partials, c->counter, it);
-            });
+            ST_TRY(halo(c, {xo}));  // the black pass reads the neighbours' red cells
+            sweep(RX_BLACK, nullptr, xo, it);
         } else {
-            timed(c, HIP_KT_RELAX, [&] {
-                hipExtLaunchKernelGGL((k_rx<16, RX_JACOBI, FL>), dim3(nb), dim3(1024), 0,
-                                      c->stream, c->ta, c->tb, 0, c->sgeo, rc, xi, xo, c->rhs,
-                                      c->rxst, c->partials, c->counter, it);
-            });
+            sweep(RX_JACOBI, xi, xo, it);
+            ST_TRY(finish(it));
         }
+        ST_TRY(halo(c, {xo}));
         hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
                               c->tb, 0, c->geo, c->rxst, nullptr, xo, 1);
+        return CFD_SUCCESS;
     };
     // iterations 0..max_iter: sweep it also yields the residual after it - 1
     // iterations, so the last launch only completes the final test
@@ -326,7 +356,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     const int chunk_max = std::max(1, c->cfg.poll_interval);
     while (it <= max_iter) {
         const int n = std::min(chunk, max_iter + 1 - it);
-        for (int q = 0; q < n; ++q, ++it) iterate(it);
+        for (int q = 0; q < n; ++q, ++it) ST_TRY(iterate(it));
         HIP_TRY(hipMemcpyAsync(&hs[slot], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost,
                                c->stream));
         HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
@@ -342,6 +372,10 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     HIP_TRY(hipStreamSynchronize(c->stream));
     flush_timing(c);
     const RxState& r = hs[2];
+    if (r.status == ST_COMM_TIMEOUT) {
+        set_err(CFD_ERROR, "relaxation: slab all-reduce timed out (a rank stopped)");
+        return CFD_ERROR;
+    }
     if (!r.done) {
         set_err(CFD_ERROR, "relaxation: device loop ended without a decision");
         return CFD_ERROR;
@@ -366,7 +400,7 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     rc.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
     rc.inv_factor = 1.0 / (2.0 * (1.0 / rc.dx2 + 1.0 / rc.dy2 + rc.inv_dz2));
     rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nzg, dx, dy, dz) : omega_in;
-    if (!dist(c) && c->sweep_ty == 16 && max_iter > 0 && !c->cfg.relax_two_pass)
+    if ((c->sweep_ty == 16 || c->sweep_ty == 8) && max_iter > 0 && !c->cfg.relax_two_pass)
         return relax_solve_fused(c, method, rc, rel_tol, abs_tol, max_iter, check_interval);
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
     const DirVals dv{};
@@ -597,6 +631,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     sg.sz = g.sz;
     sg.k0 = g.k0;
     sg.k1 = g.k1;
+    sg.kofs = g.kofs;
     sg.tiles_x = (int)((nx + 127) / 128);
     sg.tiles_y = (int)((ny + c->sweep_ty - 1) / c->sweep_ty);
     if (c->cfg.kchunk > 0) {

@@ -199,8 +199,8 @@ def test_slab_taylor_green_vs_oracle(hip_lib, nranks):
         assert float(np.max(np.abs(got[k] - ref))) / scale <= 1e-10, k
 
 
-def _slab_poisson(g, rhs, nranks, method, prm=None):
-    S = Slabs(g, nranks)
+def _slab_poisson(g, rhs, nranks, method, prm=None, check_halo=False, **cfg):
+    S = Slabs(g, nranks, **cfg)
     try:
         def body(r, c):
             sl = slice(c.k_offset, c.k_offset + c.nz_local)
@@ -212,6 +212,9 @@ def _slab_poisson(g, rhs, nranks, method, prm=None):
         for c, (s, it, xl) in zip(S.ctx, res):
             loc, glob = c.owned()
             x[glob] = xl[loc]
+        if check_halo:  # halo planes hold the neighbours' final owned planes
+            for c, (s, it, xl) in zip(S.ctx, res):
+                np.testing.assert_array_equal(xl, x[c.k_offset:c.k_offset + c.nz_local])
     finally:
         S.close()
     assert not np.isnan(x).any()
@@ -231,15 +234,23 @@ def test_slab_poisson_cg_vs_oracle(hip_lib):
 
 
 @pytest.mark.parametrize("method", [A.HIP_POISSON_REDBLACK, A.HIP_POISSON_JACOBI])
-def test_slab_poisson_relax_bitwise(hip_lib, method):
+@pytest.mark.parametrize("nranks,two_pass,maxit", [(4, 0, None), (4, 1, None), (2, 0, None),
+                                                   (3, 0, 11)])
+def test_slab_poisson_relax_bitwise(hip_lib, method, nranks, two_pass, maxit):
+    """Slab RB-SOR / Jacobi, fused device loop (residual max across ranks) and
+    two-pass form: bitwise the oracle, iteration counts and status included;
+    every rank's halo planes end equal to the neighbours' owned planes."""
     g, rhs = cases.cos_rhs(17)
     xo = np.zeros_like(rhs)
-    prm = oracle.poisson_params(max_iterations=3000 if method == A.HIP_POISSON_JACOBI else 5000)
+    if maxit is None:
+        maxit = 3000 if method == A.HIP_POISSON_JACOBI else 5000
+    prm = oracle.poisson_params(max_iterations=maxit)
     if method == A.HIP_POISSON_REDBLACK:
         so, sto = oracle.redblack_solve(xo, rhs, g.dx, g.dy, g.dz, prm)
     else:
         so, sto = oracle.jacobi_solve(xo, rhs, g.dx, g.dy, g.dz, prm)
-    stat, its, x = _slab_poisson(g, rhs, 4, method, prm)
+    stat, its, x = _slab_poisson(g, rhs, nranks, method, prm, check_halo=True,
+                                 relax_two_pass=two_pass)
     assert all(s == so for s in stat)
     assert all(i == sto.iterations for i in its)
     np.testing.assert_array_equal(x, xo)
