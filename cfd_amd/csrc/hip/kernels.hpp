@@ -1702,4 +1702,181 @@ static __global__ void k_rx_finish(RxState* st, const unsigned long long* gred, 
     if (threadIdx.x == 0 && !st->done) rx_finish(st, ord_dec_dev(gred[0]), it);
 }
 
+// ---------------------------------------------------------------------------
+// Single-pass Red-Black SOR iteration (3-D, single device): X -> Y in one
+// z-march. For plane q the tile forms R_q = X_q with its first-colour ("red",
+// (i+j+k) odd) interior cells SOR-updated (linear_solver_redblack.c:97-114);
+// then the second colour of plane q-1 is updated from R (:116-133), and the
+// L-inf residual of X at plane q (linear_solver.c:304-346) rides along. R at
+// a tile's y/x halo is recomputed locally (overlapped tiles: 128 x 16 cells
+// loaded per plane, 124 x 12 written), so each cell of X and rhs is read
+// once from HBM and Y written once: 24 B/cell per iteration instead of the
+// two colour passes' 48. R values are computed from the same X values by the
+// same expression as the first pass would, so Y is bitwise the two-pass
+// result.
+// ---------------------------------------------------------------------------
+constexpr int RB1_OX = 124;  // output columns per tile (lanes 1..62)
+constexpr int RB1_OY = 12;   // output rows per tile (waves 2..13)
+
+template <int FL>
+static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
+    SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
+    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
+    constexpr bool PF = (FL & SW_PREFETCH) != 0;
+    __shared__ double2 xb[2][16][64];  // X rows by plane parity
+    __shared__ double2 rb[2][16][64];  // R rows by plane parity
+    __shared__ double sh[16];
+    __shared__ int flag;
+    if (st->done) return;
+    const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
+    const int t = xcd_tile(blockIdx.x, nt);
+    const int tx = t % g.tiles_x;
+    const int rest = t / g.tiles_x;
+    const int ty = rest % g.tiles_y;
+    const int tz = rest / g.tiles_y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i0 = tx * RB1_OX - 2 + 2 * lane;  // even; the pair is (i0, i0 + 1)
+    const int j = ty * RB1_OY - 2 + w;
+    const int kb = g.k0 + tz * g.kc;
+    const int ke = min(kb + g.kc, g.k1);
+    const bool ld = (j >= 0 && j < g.ny && i0 >= 0 && i0 < g.nx);
+    const bool jin = (j >= 1 && j <= g.ny - 2);
+    const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;
+    const bool in1 = jin && i0 + 1 <= g.nx - 2;  // i0 + 1 >= 1 always
+    const bool ownrow = (w >= 2 && w < 2 + RB1_OY);
+    const bool own = ownrow && (lane >= 1 && lane <= 62);
+    const bool rrow = (w >= 1 && w <= 14);
+    const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
+    const double2 zero = make_double2(0.0, 0.0);
+    auto ldx = [&](int k) -> double2 {
+        return (ld && k >= 0 && k < g.nz) ? ld2(X, (long long)k * g.ps + col) : make_double2(0.0, 0.0);
+    };
+    auto ldr = [&](int k) -> double2 {
+        return (ld && k >= 0 && k < g.nz) ? ld2v<FL>(rhs, (long long)k * g.ps + col)
+                                          : make_double2(0.0, 0.0);
+    };
+    // step q forms R_{q+1} and updates the second colour of plane q.
+    // Registers: X_q, X_{q+1}, X_{q+2} (xm, xc, xp); R_{q-1}, R_q (rmm, rm);
+    // rhs_{q+1}, rhs_q (bq, bm). LDS at the top of step q: X_{q+1} rows in
+    // xb[(q+1)&1], R_q rows in rb[q&1]; one barrier per plane.
+    int q = kb - 2;
+    double2 xm = ldx(q), xc = ldx(q + 1), xp = ldx(q + 2);
+    double2 bq = ldr(q + 1), bm = zero, rmm = zero, rm = zero;
+    double2 nx_x = PF ? ldx(q + 3) : zero, nx_b = PF ? ldr(q + 2) : zero;
+    xb[(q + 1) & 1][w][lane] = xc;
+    double m = 0.0;
+    for (; q < ke; ++q) {
+        double2 fx = zero, fb = zero;  // X_{q+3}, rhs_{q+2}
+        if (PF) {
+            fx = nx_x;
+            fb = nx_b;
+            if (q + 1 < ke) {
+                nx_x = ldx(q + 4);
+                nx_b = ldr(q + 3);
+            }
+        }
+        __syncthreads();
+        const int qa = q + 1;
+        // ---- R_{q+1} and the residual of X at plane q+1 ----
+        const bool qin = (qa >= g.k0 && qa < g.k1);
+        double2 R = xc;
+        if (rrow) {
+            const double2 ys = xb[qa & 1][w - 1][lane];
+            const double2 yn = xb[qa & 1][w + 1][lane];
+            const double left = __shfl_up(xc.y, 1, 64);
+            const double right = __shfl_down(xc.x, 1, 64);
+            const bool first = ((j + qa + g.kofs) & 1) == 1;  // cell i0 has the odd parity
+            const double vc = first ? xc.x : xc.y;
+            const double vl = first ? left : xc.x, vr = first ? xc.y : right;
+            const double vs = first ? ys.x : ys.y, vn = first ? yn.x : yn.y;
+            const double vm = first ? xm.x : xm.y, vp = first ? xp.x : xp.y;
+            const double vb = first ? bq.x : bq.y;
+            if (qin && (first ? in0 : in1)) {
+                const double pn = -(vb - (vr + vl) / rc.dx2 - (vn + vs) / rc.dy2 -
+                                    (vp + vm) * rc.inv_dz2) *
+                                  rc.inv_factor;
+                const double xn = vc + rc.omega * (pn - vc);
+                if (first) R.x = xn;
+                else R.y = xn;
+            }
+            if (own && qin && qa >= kb && qa < ke) {
+                const double l0 = (xc.y - 2.0 * xc.x + left) / rc.dx2 +
+                                  (yn.x - 2.0 * xc.x + ys.x) / rc.dy2 +
+                                  (xp.x + xm.x - 2.0 * xc.x) * rc.inv_dz2;
+                const double l1 = (right - 2.0 * xc.y + xc.x) / rc.dx2 +
+                                  (yn.y - 2.0 * xc.y + ys.y) / rc.dy2 +
+                                  (xp.y + xm.y - 2.0 * xc.y) * rc.inv_dz2;
+                const double r0 = fabs(l0 - bq.x), r1 = fabs(l1 - bq.y);
+                if (in0 && r0 > m) m = r0;
+                if (in1 && r1 > m) m = r1;
+            }
+        }
+        // ---- second colour of plane q from R_{q-1}, R_q, R_{q+1} ----
+        if (q >= kb && ownrow) {  // wave-uniform: shuffles below
+            const double2 ys = rb[q & 1][w - 1][lane];
+            const double2 yn = rb[q & 1][w + 1][lane];
+            const double left = __shfl_up(rm.y, 1, 64);
+            const double right = __shfl_down(rm.x, 1, 64);
+            const bool first = ((j + q + g.kofs) & 1) == 0;  // cell i0 has the even parity
+            const double vc = first ? rm.x : rm.y;
+            const double vl = first ? left : rm.x, vr = first ? rm.y : right;
+            const double vs = first ? ys.x : ys.y, vn = first ? yn.x : yn.y;
+            const double vm = first ? rmm.x : rmm.y, vp = first ? R.x : R.y;
+            const double vb = first ? bm.x : bm.y;
+            double2 out = rm;
+            if (own && (first ? in0 : in1)) {
+                const double pn = -(vb - (vr + vl) / rc.dx2 - (vn + vs) / rc.dy2 -
+                                    (vp + vm) * rc.inv_dz2) *
+                                  rc.inv_factor;
+                const double xn = vc + rc.omega * (pn - vc);
+                if (first) out.x = xn;
+                else out.y = xn;
+            }
+            if (own && ld && jin) st2v<FL>(Y, (long long)q * g.ps + col, out);
+        }
+        rmm = rm;
+        rm = R;
+        bm = bq;
+        xm = xc;
+        xc = xp;
+        if (PF) {
+            xp = fx;
+            bq = fb;
+        } else {
+            xp = ldx(q + 3);
+            bq = ldr(q + 2);
+        }
+        // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were last
+        // read in step q - 1, before this step's barrier)
+        xb[(q + 2) & 1][w][lane] = xc;
+        rb[(q + 1) & 1][w][lane] = rm;
+    }
+    m = wave_max(m);
+    if (lane == 0) sh[w] = m;
+    __syncthreads();
+    double* shs = (double*)&xb[0][0][0];
+    if (threadIdx.x == 0) {
+        double a = 0.0;
+        for (int v = 0; v < 16; ++v) a = fmax(a, sh[v]);
+        store_sc1(&partials[blockIdx.x], a);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned tk = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        flag = (tk == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (flag == 0) return;
+    double a = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 1024) a = fmax(a, load_sc1(&partials[b]));
+    a = wave_max(a);
+    if (lane == 0) shs[w] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = 0.0;
+        for (int v = 0; v < 16; ++v) tot = fmax(tot, shs[v]);
+        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rx_finish(st, tot, it);
+    }
+}
+
 }  // namespace cfdhip

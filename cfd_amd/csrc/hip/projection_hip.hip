@@ -324,6 +324,11 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                               c->rxst, gred, it);
         return CFD_SUCCESS;
     };
+    // one-pass RB-SOR (k_rb1) on a single device in 3-D; relax_two_pass = 2
+    // forces the two colour sweeps of k_rx
+    const bool single = method == HIP_POISSON_REDBLACK && !D && c->nz > 1 &&
+                        c->cfg.relax_two_pass == 0;
+    const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
     ST_TRY(halo(c, {c->pn}));
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
                           rel_tol, abs_tol, max_iter, check_interval);
@@ -333,7 +338,13 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     auto iterate = [&](int it) -> cfd_status_t {
         double* xi = X[it & 1];
         double* xo = X[(it + 1) & 1];
-        if (method == HIP_POISSON_REDBLACK) {
+        if (single) {
+            timed(c, HIP_KT_RELAX, [&] {
+                hipExtLaunchKernelGGL((k_rb1<FL>), dim3(nb1), dim3(1024), 0, c->stream, c->ta,
+                                      c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst,
+                                      c->partials, c->counter, it);
+            });
+        } else if (method == HIP_POISSON_REDBLACK) {
             sweep(RX_RED, xi, xo, it);
             ST_TRY(finish(it));
             hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream,
@@ -400,7 +411,7 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     rc.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
     rc.inv_factor = 1.0 / (2.0 * (1.0 / rc.dx2 + 1.0 / rc.dy2 + rc.inv_dz2));
     rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nzg, dx, dy, dz) : omega_in;
-    if ((c->sweep_ty == 16 || c->sweep_ty == 8) && max_iter > 0 && !c->cfg.relax_two_pass)
+    if ((c->sweep_ty == 16 || c->sweep_ty == 8) && max_iter > 0 && c->cfg.relax_two_pass != 1)
         return relax_solve_fused(c, method, rc, rel_tol, abs_tol, max_iter, check_interval);
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
     const DirVals dv{};
@@ -649,6 +660,20 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     sg.kc = std::max(1, std::min(sg.kc, nint_k));
     sg.tiles_z = (nint_k + sg.kc - 1) / sg.kc;
     int n_partials = std::max(c->grid_cap, sg.tiles_x * sg.tiles_y * sg.tiles_z);
+    // single-pass RB-SOR tiling (k_rb1): 124 x 12 cells written per 128 x 16 loaded
+    {
+        SGeo& rg = c->rgeo;
+        rg = sg;
+        rg.tiles_x = (int)((nx + RB1_OX - 1) / RB1_OX);
+        rg.tiles_y = (int)((ny + RB1_OY - 1) / RB1_OY);
+        rg.kc = 64;
+        while (rg.kc > 16 &&
+               (long long)rg.tiles_x * rg.tiles_y * ((nint_k + rg.kc - 1) / rg.kc) < 512)
+            rg.kc /= 2;
+        rg.kc = std::max(1, std::min(rg.kc, nint_k));
+        rg.tiles_z = (nint_k + rg.kc - 1) / rg.kc;
+        n_partials = std::max(n_partials, rg.tiles_x * rg.tiles_y * rg.tiles_z);
+    }
     c->split_b = (c->nranks > 1 && nint_k >= 3) ? 1 : 0;
     if (c->split_b) {
         // sweep B on slabs: the two edge planes (what the neighbours need)

@@ -76,9 +76,11 @@ typedef struct {
                                      (solver_projection.c:220-224, default); 0: the step
                                      continues with the capped solve, as the reference GPU
                                      does (solver_projection_gpu.cu:717-733) */
-    int relax_two_pass;           /* RB-SOR / Jacobi: 1 = separate colour passes + residual
-                                     pass with a host check per iteration (the r01 form);
-                                     0 = fused device loop (default, single device) */
+    int relax_two_pass;           /* RB-SOR / Jacobi: 0 = device loop, RB-SOR in one pass per
+                                     iteration where possible (3-D, one device; default);
+                                     1 = separate colour passes + residual pass with a host
+                                     check per iteration (the r01 form); 2 = device loop with
+                                     the two colour sweeps */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;

@@ -242,10 +242,12 @@ def test_poisson_relax_bitwise(hip_lib, method):
     ((33, 29, 1), dict(check_interval=5)),                    # 2-D, sparse checks
     ((130, 20, 9), dict(max_iterations=40, check_interval=3)),  # two x tiles, odd ny
     ((17, 17, 17), dict(tolerance=1e-2)),                     # early stop, odd iterate
+    ((250, 30, 40), dict(max_iterations=25)),                 # 3x3 one-pass tiles, z chunks
 ])
 def test_poisson_relax_fused_loop_bitwise(hip_lib, method, shape, kw):
-    """The fused device loop (k_rx, lagged residual, ping-pong buffers) and
-    the two-pass form both equal the oracle bit for bit: iterate, iteration
+    """The device loop (one-pass RB k_rb1 or the two colour sweeps of k_rx,
+    lagged residual, ping-pong buffers) and the host two-pass form all equal
+    the oracle bit for bit: iterate, iteration
     count (max_iterations + 1 when capped, linear_solver.c:472), status,
     initial and final residual."""
     nx, ny, nz = shape
@@ -262,7 +264,7 @@ def test_poisson_relax_fused_loop_bitwise(hip_lib, method, shape, kw):
         so, sto = oracle.redblack_solve(xo, rhs, d, d, dz, prm)
     else:
         so, sto = oracle.jacobi_solve(xo, rhs, d, d, dz, prm)
-    for two_pass in (0, 1):
+    for two_pass in (0, 1, 2):  # one-pass RB (3-D) / host two-pass / device two-colour
         ctx = api.HipProjection(nx, ny, nz, relax_two_pass=two_pass)
         xh = x0.copy()
         sh, sth = ctx.poisson_solve(method, xh, rhs, d, d, dz, prm)

@@ -43,8 +43,9 @@ def main():
     tb.left = tb.right = A.BC_TYPE_DIRICHLET
     tb.top = tb.bottom = tb.front = tb.back = A.BC_TYPE_NEUMANN
     tb.dirichlet_values.left, tb.dirichlet_values.right = T_hot, T_cold
+    mode = int(os.environ.get("RELAX_MODE", "0"))  # hip_proj_config_t.relax_two_pass
     ctx = api.HipProjection(nx, nx, nz, poisson_method=A.HIP_POISSON_REDBLACK,
-                             poisson_max_iter=maxit)
+                             poisson_max_iter=maxit, relax_two_pass=mode)
     for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
         ctx.fill(fid, 0.0)
     x = np.asarray(g.x)
@@ -71,6 +72,7 @@ def main():
     rb_iter_ms = rms / iters if iters else None   # red + black sweeps per iteration
     print(json.dumps({
         "workload": f"{nx}x{nx}x{nz} natural convection Ra=1e3, projection_hip RB-SOR, 1 GPU",
+        "relax_mode": mode,
         "steps": steps, "rbsor_iters_per_step": its, "ms_per_step": round(el / steps * 1e3, 1),
         "MLUPS": round(cells * steps / el / 1e6, 3),
         "rbsor_iter_ms": round(rb_iter_ms, 4) if rb_iter_ms else None,
