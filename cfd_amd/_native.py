@@ -184,6 +184,17 @@ def _bind_hip(lib) -> None:
     _sig(lib, "create_rk4_hip_solver", P(A.NSSolver))
     _sig(lib, "cfd_hip_register_solvers", None, V)
     _sig(lib, "hip_proj_write_vtk", C.c_int, V, C.c_char_p, P(A.Grid), C.c_double)
+    # boundary_conditions_gpu.h (device pointers, packed layout, opaque stream)
+    _sig(lib, "bc_apply_neumann_gpu", None, V, C.c_size_t, C.c_size_t, V)
+    _sig(lib, "bc_apply_scalar_gpu", None, V, C.c_size_t, C.c_size_t, C.c_int, V)
+    _sig(lib, "bc_apply_velocity_gpu", None, V, V, C.c_size_t, C.c_size_t, C.c_int, V)
+    _sig(lib, "bc_apply_dirichlet_scalar_gpu", None, V, C.c_size_t, C.c_size_t,
+         P(A.DirichletValues), V)
+    _sig(lib, "bc_apply_dirichlet_velocity_gpu", None, V, V, C.c_size_t, C.c_size_t,
+         P(A.DirichletValues), P(A.DirichletValues), V)
+    _sig(lib, "bc_apply_scalar_3d_gpu", None, V, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, V)
+    _sig(lib, "bc_apply_velocity_3d_gpu", None, V, V, V, C.c_size_t, C.c_size_t, C.c_size_t,
+         C.c_int, V)
     _sig(lib, "create_cg_gpu_solver", P(A.PoissonSolver))
     _sig(lib, "create_redblack_gpu_solver", P(A.PoissonSolver))
     _sig(lib, "create_jacobi_gpu_solver", P(A.PoissonSolver))

@@ -44,6 +44,15 @@ def test_hip_library_exports_gpu_device_api():
     assert not missing, missing
 
 
+def test_hip_library_exports_device_bc_api():
+    """boundary_conditions_gpu.cuh:32-151 entry points (inlet excepted)."""
+    _native.hip()
+    names = _declared(INC / "boundary_conditions_gpu.h")
+    assert len(names) == 7
+    missing = set(names) - _exported(_native.HIP_LIB)
+    assert not missing, missing
+
+
 def test_host_library_exports_host_api():
     _native.host()
     names = _declared(INC / "cfd_host.h")
