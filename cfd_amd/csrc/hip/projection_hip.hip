@@ -648,11 +648,12 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     if (c->cfg.kchunk > 0) {
         sg.kc = c->cfg.kchunk;
     } else {
-        // 64-plane z runs, shortened (down to 16) until the launch has
-        // enough wavefronts for full occupancy (32 per CU): a thin slab must
-        // still fill all 256 CUs
-        sg.kc = 64;
-        const long long want = 32LL * (c->grid_cap / 8) / c->sweep_ty;
+        // long z runs (each chunk re-reads two planes), shortened (down to
+        // 16) until every CU has a workgroup: a thin slab must still fill
+        // all 256 CUs. r01f at 512^3: 256-plane runs (256 workgroups) beat
+        // 64 by ~2 %; one 8-rank slab: 32 beat 16 (profiles/r01f_sweep_*)
+        sg.kc = 256;
+        const long long want = c->grid_cap / 8;
         while (sg.kc > 16 &&
                (long long)sg.tiles_x * sg.tiles_y * ((nint_k + sg.kc - 1) / sg.kc) < want)
             sg.kc /= 2;
