@@ -138,6 +138,7 @@ class HipProjConfig(C.Structure):
         ("sor_omega", C.c_double), ("poll_interval", C.c_int), ("kchunk", C.c_int),
         ("verbose", C.c_int), ("sweep_rows", C.c_int), ("sweep_variant", C.c_int),
         ("rhs_density", C.c_int), ("poisson_fail_fatal", C.c_int), ("relax_two_pass", C.c_int),
+        ("sweep_variant_fold", C.c_int),
     ]
 
 

@@ -64,6 +64,7 @@ struct hip_proj_ctx {
     int split_b = 0;
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
     int sweep_variant = 0;  // SW_NT_* flags of the CG sweeps
+    int sweep_variant_fold = 0;  // the fold sweep's flags (0: sweep_variant)
     int grid_cap = 2048;
     hip_proj_config_t cfg{};
     // Z-slab decomposition (nranks == 1: the whole grid, no communicator)

@@ -100,7 +100,21 @@ static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* 
     return launch_cgA_v<8>(c, first, L, r, po, pn, it);
 }
 
+// the fold sweep (it % 4 == 3) may use its own memory-hint variant (16-row tiles)
+template <int FL>
+static void launch_cgBX(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
+    if (dist(c)) launch_cgB_t<16, true, FL, true>(c, sg, L, a, it);
+    else launch_cgB_t<16, false, FL, true>(c, sg, L, a, it);
+}
+
 static void launch_cgB(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
+    if (c->sweep_ty == 16 && (it % CG_XFOLD) == CG_XFOLD - 1 && c->sweep_variant_fold) {
+        switch (c->sweep_variant_fold) {
+            case 3: return launch_cgBX<3>(c, sg, L, a, it);
+            case 11: return launch_cgBX<11>(c, sg, L, a, it);
+            default: return launch_cgBX<15>(c, sg, L, a, it);
+        }
+    }
     if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, sg, L, a, it);
     if (c->sweep_ty == 16) return launch_cgB_v<16>(c, sg, L, a, it);
     return launch_cgB_v<8>(c, sg, L, a, it);
@@ -552,6 +566,7 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.rhs_density = 1;
     c.poisson_fail_fatal = 1;
     c.relax_two_pass = 0;
+    c.sweep_variant_fold = 0;
     return c;
 }
 
@@ -632,6 +647,10 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         if (v == 15 && c->sweep_ty >= 8) c->sweep_variant = v;
         else if ((v == 23 || v == 31) && c->sweep_ty == 16) c->sweep_variant = v;
         else c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : (v & 3);
+    }
+    {
+        const int vf = c->cfg.sweep_variant_fold;
+        c->sweep_variant_fold = (c->sweep_ty == 16 && (vf == 3 || vf == 11 || vf == 15)) ? vf : 0;
     }
     SGeo& sg = c->sgeo;
     sg.nx = g.nx;

@@ -81,6 +81,8 @@ typedef struct {
                                      1 = separate colour passes + residual pass with a host
                                      check per iteration (the r01 form); 2 = device loop with
                                      the two colour sweeps */
+    int sweep_variant_fold;       /* memory hints of the x-folding sweep B (every 4th CG
+                                     iteration, 16-row tiles): 0 = sweep_variant; 3, 11, 15 */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
