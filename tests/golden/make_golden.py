@@ -94,8 +94,42 @@ def dvd_ra1e3():
     np.savez_compressed(HERE / "dvd41_ra1e3_fields.npz", u=f.u, v=f.v, p=f.p, T=f.T)
 
 
+def cavity128_re1000(steps=100000, snap=1000):
+    """BASELINE configs[0]: 128x128x1 lid-driven cavity, Re=1000, dt=5e-4,
+    100 000 steps (t = 50, test_cavity_backends.c:74-76), scalar projection
+    with the cavity BCs before every step (lid_driven_cavity_common.h:238-270).
+    Writes the Ghia RMS (cavity_validation_utils.h:36-65 restated in
+    tests/ghia.py), the centrelines, the per-step CG iteration counts and the
+    fields after `snap` steps and at the end. About an hour on one core."""
+    import json
+
+    from tests import ghia
+    g, f, p = cases.cavity(128, 128, 1, Re=1000.0, dt=5e-4)
+    its = []
+    for n in range(1, steps + 1):
+        api.cavity_bc(f, 1.0)
+        s, st, it = oracle.projection_step(f, g, p)
+        assert s == A.CFD_SUCCESS
+        its.append(it)
+        if n == snap:
+            np.savez_compressed(HERE / f"cavity128_re1000_{snap}steps.npz",
+                                iters=np.array(its), **fields(f))
+    api.cavity_bc(f, 1.0)
+    y, uc, x, vc = ghia.centerlines(f.u[0], f.v[0], g.x, g.y)
+    rms_u, rms_v = ghia.rms_errors(f, g, 1000)
+    r = {"steps": steps, "dt": 5e-4, "re": 1000.0, "rms_u": rms_u, "rms_v": rms_v,
+         "cg_iters_total": int(sum(its)), "cg_iters_last": int(its[-1]),
+         "u_centerline": uc, "v_centerline": vc}
+    (HERE / "cavity128_re1000_t50.json").write_text(json.dumps(r, indent=1) + "\n")
+    np.savez_compressed(HERE / "cavity128_re1000_t50_fields.npz",
+                        iters=np.array(its, dtype=np.int32), **fields(f))
+
+
 if __name__ == "__main__":
     oracle.set_threads(1)
+    if sys.argv[1:] == ["cavity128"]:
+        cavity128_re1000()
+        sys.exit(0)
     dvd_ra1e3()
     kat()
     cavity_rbsor()
