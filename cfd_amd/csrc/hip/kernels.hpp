@@ -1360,7 +1360,24 @@ static __global__ __launch_bounds__(256) void k_vel_stats(Geo g, const double* _
 // ---------------------------------------------------------------------------
 struct RelaxCoef {
     double dx2, dy2, inv_dz2, inv_factor, omega;
+    double rdx2, rdy2;  // RN(1 / dx2), RN(1 / dy2) for divc
 };
+
+// a / d, correctly rounded, for the constant divisors dx2 / dy2 of the
+// relaxation sweeps, from the correctly rounded reciprocal r = RN(1/d):
+// q = RN(a r) is within 1 ulp of a/d, a - q d is exact in one FMA, and the
+// corrected q + (a - q d) r rounds to RN(a/d) (Markstein's correction, the
+// IA-64 division scheme) -- 3 VALU ops instead of the ~14-op generic fp64
+// division, bitwise the reference's `/` (checked on 9.6e8 random quotients,
+// tools/divc_check.c, and by the bitwise relaxation tests). Quotients near the
+// underflow/overflow range, zeros (sign of zero) and non-finite values take
+// the generic division.
+__device__ __forceinline__ double divc(double a, double d, double r) {
+    const double q = a * r;
+    const double aq = fabs(q);
+    if (!(aq >= 0x1p-900 && aq <= 0x1p+900)) return a / d;  // residual stays normal
+    return fma(fma(-q, d, a), r, q);
+}
 
 static __global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __restrict__ x,
                                                 const double* __restrict__ rhs, int parity) {
@@ -1605,11 +1622,11 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
         if (c.lane == 63) right = cur.el;
         // cell 0: (xm, xp) = (left, pc.y); cell 1: (pc.x, right)
         if (RES) {  // linear_solver.c:304-346 (k_residual_linf's expression)
-            const double l0 = (pc.y - 2.0 * pc.x + left) / rc.dx2 +
-                              (yn.x - 2.0 * pc.x + ys.x) / rc.dy2 +
+            const double l0 = divc(pc.y - 2.0 * pc.x + left, rc.dx2, rc.rdx2) +
+                              divc(yn.x - 2.0 * pc.x + ys.x, rc.dy2, rc.rdy2) +
                               (pp.x + pm.x - 2.0 * pc.x) * rc.inv_dz2;
-            const double l1 = (right - 2.0 * pc.y + pc.x) / rc.dx2 +
-                              (yn.y - 2.0 * pc.y + ys.y) / rc.dy2 +
+            const double l1 = divc(right - 2.0 * pc.y + pc.x, rc.dx2, rc.rdx2) +
+                              divc(yn.y - 2.0 * pc.y + ys.y, rc.dy2, rc.rdy2) +
                               (pp.y + pm.y - 2.0 * pc.y) * rc.inv_dz2;
             const double r0 = fabs(l0 - cur.rr.x), r1 = fabs(l1 - cur.rr.y);
             if (c.in0 && r0 > m) m = r0;
@@ -1617,10 +1634,12 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
         }
         double2 out = pc;
         if (MODE == RX_JACOBI) {
-            const double pn0 = -(cur.rr.x - (pc.y + left) / rc.dx2 - (yn.x + ys.x) / rc.dy2 -
+            const double pn0 = -(cur.rr.x - divc(pc.y + left, rc.dx2, rc.rdx2) -
+                                 divc(yn.x + ys.x, rc.dy2, rc.rdy2) -
                                  (pp.x + pm.x) * rc.inv_dz2) *
                                rc.inv_factor;
-            const double pn1 = -(cur.rr.y - (right + pc.x) / rc.dx2 - (yn.y + ys.y) / rc.dy2 -
+            const double pn1 = -(cur.rr.y - divc(right + pc.x, rc.dx2, rc.rdx2) -
+                                 divc(yn.y + ys.y, rc.dy2, rc.rdy2) -
                                  (pp.y + pm.y) * rc.inv_dz2) *
                                rc.inv_factor;
             if (c.in0) out.x = pn0;
@@ -1634,7 +1653,8 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_rx(
             const double yl = first ? ys.x : ys.y, yr = first ? yn.x : yn.y;
             const double zl = first ? pm.x : pm.y, zr = first ? pp.x : pp.y;
             const double rh = first ? cur.rr.x : cur.rr.y;
-            const double pn = -(rh - (xr + xl) / rc.dx2 - (yr + yl) / rc.dy2 - (zr + zl) * rc.inv_dz2) *
+            const double pn = -(rh - divc(xr + xl, rc.dx2, rc.rdx2) -
+                                divc(yr + yl, rc.dy2, rc.rdy2) - (zr + zl) * rc.inv_dz2) *
                               rc.inv_factor;
             const double xn = xc + rc.omega * (pn - xc);
             if (first) {
@@ -1792,7 +1812,8 @@ static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
             const double vm = first ? xm.x : xm.y, vp = first ? xp.x : xp.y;
             const double vb = first ? bq.x : bq.y;
             if (qin && (first ? in0 : in1)) {
-                const double pn = -(vb - (vr + vl) / rc.dx2 - (vn + vs) / rc.dy2 -
+                const double pn = -(vb - divc(vr + vl, rc.dx2, rc.rdx2) -
+                                    divc(vn + vs, rc.dy2, rc.rdy2) -
                                     (vp + vm) * rc.inv_dz2) *
                                   rc.inv_factor;
                 const double xn = vc + rc.omega * (pn - vc);
@@ -1800,11 +1821,11 @@ static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
                 else R.y = xn;
             }
             if (own && qin && qa >= kb && qa < ke) {
-                const double l0 = (xc.y - 2.0 * xc.x + left) / rc.dx2 +
-                                  (yn.x - 2.0 * xc.x + ys.x) / rc.dy2 +
+                const double l0 = divc(xc.y - 2.0 * xc.x + left, rc.dx2, rc.rdx2) +
+                                  divc(yn.x - 2.0 * xc.x + ys.x, rc.dy2, rc.rdy2) +
                                   (xp.x + xm.x - 2.0 * xc.x) * rc.inv_dz2;
-                const double l1 = (right - 2.0 * xc.y + xc.x) / rc.dx2 +
-                                  (yn.y - 2.0 * xc.y + ys.y) / rc.dy2 +
+                const double l1 = divc(right - 2.0 * xc.y + xc.x, rc.dx2, rc.rdx2) +
+                                  divc(yn.y - 2.0 * xc.y + ys.y, rc.dy2, rc.rdy2) +
                                   (xp.y + xm.y - 2.0 * xc.y) * rc.inv_dz2;
                 const double r0 = fabs(l0 - bq.x), r1 = fabs(l1 - bq.y);
                 if (in0 && r0 > m) m = r0;
@@ -1825,7 +1846,8 @@ static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
             const double vb = first ? bm.x : bm.y;
             double2 out = rm;
             if (own && (first ? in0 : in1)) {
-                const double pn = -(vb - (vr + vl) / rc.dx2 - (vn + vs) / rc.dy2 -
+                const double pn = -(vb - divc(vr + vl, rc.dx2, rc.rdx2) -
+                                    divc(vn + vs, rc.dy2, rc.rdy2) -
                                     (vp + vm) * rc.inv_dz2) *
                                   rc.inv_factor;
                 const double xn = vc + rc.omega * (pn - vc);

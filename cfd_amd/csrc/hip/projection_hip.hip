@@ -425,6 +425,8 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     rc.inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
     rc.inv_factor = 1.0 / (2.0 * (1.0 / rc.dx2 + 1.0 / rc.dy2 + rc.inv_dz2));
     rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nzg, dx, dy, dz) : omega_in;
+    rc.rdx2 = 1.0 / rc.dx2;
+    rc.rdy2 = 1.0 / rc.dy2;
     if ((c->sweep_ty == 16 || c->sweep_ty == 8) && max_iter > 0 && c->cfg.relax_two_pass != 1)
         return relax_solve_fused(c, method, rc, rel_tol, abs_tol, max_iter, check_interval);
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
