@@ -4,7 +4,9 @@
  * n = 17 .. 1025 points on domains of length 1, 2*pi and 0.5, over random a
  * of either sign with exponents in [-60, 60] (2e7 quotients per divisor).
  *   gcc -O2 -ffp-contract=off -o /tmp/divc_check tools/divc_check.c -lm && /tmp/divc_check
- * Prints the number of mismatches (0 expected) and exits 1 on any. */
+ * Optional argv[1]: quotients per divisor. Prints the number of mismatches
+ * (0 expected) and exits 1 on any. */
+#include <stdlib.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -18,7 +20,8 @@ static inline uint64_t xorshift(void) {
     return s;
 }
 
-int main(void) {
+int main(int argc, char** argv) {
+    const long per = argc > 1 ? atol(argv[1]) : 20000000;
     const int ns[] = {17, 24, 32, 33, 41, 64, 65, 100, 128, 129, 256, 257, 512, 1000, 1024, 1025};
     const double lens[] = {1.0, 2.0 * M_PI, 0.5};
     long bad = 0, tot = 0;
@@ -26,7 +29,7 @@ int main(void) {
         for (int dom = 0; dom < 3; dom++) {
             const double dx = lens[dom] / (ns[t] - 1);
             const double d = dx * dx, r = 1.0 / d;
-            for (long n = 0; n < 20000000; n++) {
+            for (long n = 0; n < per; n++) {
                 const uint64_t b = xorshift();
                 const uint64_t e = 1023 - 60 + (b >> 52) % 121;
                 const uint64_t bits = (b & 0x000FFFFFFFFFFFFFull) | (e << 52) | ((xorshift() & 1) << 63);
