@@ -58,3 +58,30 @@ def test_poisson_fixture_regenerates_bitwise():
     s, st = oracle.redblack_solve(x, rhs, g.dx, g.dy, g.dz)
     assert st.iterations == z["iters_rbsor"]
     np.testing.assert_array_equal(x, z["x_rbsor"])
+
+
+def test_cavity128_re1000_fixture_consistent():
+    """configs[0] oracle fixture (make_golden.py cavity128): the Ghia RMS the
+    survey measured on a reference build (0.0299 / 0.0282),
+    under the reference's 0.10 gate (test_cavity_backends.c:50), and the
+    stored centrelines / fields agree with each other; the first 10 steps of
+    the 1000-step snapshot are re-run on the oracle here."""
+    from tests import ghia
+    r = json.loads((GOLD / "cavity128_re1000_t50.json").read_text())
+    assert round(r["rms_u"], 4) == 0.0299 and round(r["rms_v"], 4) == 0.0282
+    assert r["rms_u"] < 0.10 and r["rms_v"] < 0.10
+    z = load("cavity128_re1000_t50_fields.npz")
+    g = api.Grid(128, 128, 1, 0.0, 1.0, 0.0, 1.0, 0.0, 0.0)
+    y, uc, x, vc = ghia.centerlines(z["u"][0], z["v"][0], g.x, g.y)
+    assert uc == r["u_centerline"] and vc == r["v_centerline"]
+    assert int(z["iters"].sum()) == r["cg_iters_total"]
+    snap = load("cavity128_re1000_1000steps.npz")
+    assert np.array_equal(snap["iters"], z["iters"][:1000])
+    g, f, p = cases.cavity(128, 128, 1, Re=1000.0, dt=5e-4)
+    its = []
+    for _ in range(10):
+        api.cavity_bc(f, 1.0)
+        s, _, it = oracle.projection_step(f, g, p)
+        assert s == A.CFD_SUCCESS
+        its.append(it)
+    assert its == list(snap["iters"][:10])
