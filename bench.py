@@ -35,7 +35,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # 2*FETCH_SIZE + WRITE_SIZE per working launch of sweep A, the gfx950
 # correction of MI355X_MICROARCH.md "HBM [CDNA4]".
 # Newest first; the first file that holds the kernel being reported is used.
-TRAFFIC_JSONS = [ROOT / "profiles" / "r01g_traffic_cg_sweeps.json",
+TRAFFIC_JSONS = [ROOT / "profiles" / "r01h_traffic_cg_sweeps.json",
+                 ROOT / "profiles" / "r01g_traffic_cg_sweeps.json",
                  ROOT / "profiles" / "r01f_traffic_cg_sweeps.json",
                  ROOT / "profiles" / "r01e_traffic_cg_sweeps.json",
                  ROOT / "profiles" / "r01c_traffic_cg_sweeps.json"]
