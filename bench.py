@@ -284,6 +284,17 @@ def pmc_traffic(kname, cells):
     return None, None
 
 
+def host_cpu_model():
+    """`model name` of /proc/cpuinfo (record the host CPU)."""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(n, args, k_gpu):
     """The oracle (OpenMP port of the reference projection) timed on this host
     on a bounded sample of the same step: predictor, divergence and corrector in
@@ -326,7 +337,8 @@ def cpu_baseline(n, args, k_gpu):
                       f"in full, {it} CG iterations timed ({t_cg_iter*1e3:.1f} ms/iter) and "
                       f"scaled to the GPU's {k_gpu:.0f} iterations/step; OpenMP x{threads}; "
                       f"sample wall {wall:.1f} s"),
-           "cg_iter_ms": round(t_cg_iter * 1e3, 2), "status": s}
+           "cg_iter_ms": round(t_cg_iter * 1e3, 2), "status": s,
+           "host_cpu_model": host_cpu_model(), "host_cpus": os.cpu_count()}
     if args.cpu_scalar_cg_iters > 0:
         # the scalar reference configuration: one thread
         s1, it1, wall1, t1_cg, t1_step = sample(1, args.cpu_scalar_cg_iters)
