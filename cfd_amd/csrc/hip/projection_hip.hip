@@ -689,6 +689,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         rg.tiles_x = (int)((nx + RB1_OX - 1) / RB1_OX);
         rg.tiles_y = (int)((ny + RB1_OY - 1) / RB1_OY);
         rg.kc = 64;
+        if (const char* e = getenv("CFD_HIP_RB1_KC")) rg.kc = std::max(1, atoi(e));  // experiments
         while (rg.kc > 16 &&
                (long long)rg.tiles_x * rg.tiles_y * ((nint_k + rg.kc - 1) / rg.kc) < 512)
             rg.kc /= 2;
