@@ -401,3 +401,28 @@ def test_ghia_33_re100_device_resident(hip_lib):
     assert round(rms_u, 4) == 0.0382
     assert abs(rms_v - 0.0440) < 0.001
     ctx.close()
+
+
+def test_tg3d_32_device_resident_l2_vs_oracle(hip_lib):
+    """BASELINE configs[1] at test size: Taylor-Green 32^3, 100 steps, fields
+    resident in HBM with the periodic BCs applied on the device before every
+    step. The relative L2 errors against the analytic decay match the oracle's
+    to 1e-9 (CG dot order only) and pass the reference's TG3_L2_ERROR_TOL =
+    0.25 (taylor_green_3d_reference.h:58)."""
+    g, f, p = cases.tg3(32)
+    ctx = api.HipProjection(32, 32, 32)
+    ctx.upload(f)
+    for _ in range(100):
+        for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
+            ctx.apply_scalar_bc(fid, A.BC_TYPE_PERIODIC)
+        assert ctx.step_device(g, p) == A.CFD_SUCCESS, api._native.last_error()
+    ctx.download(f)
+    ctx.close()
+    eu, ev = cases.tg3_l2_errors(g, f, 100 * 1e-3)
+    go, fo, po = cases.tg3(32)
+    for _ in range(100):
+        cases.tg3_bc(fo)
+        assert oracle.projection_step(fo, go, po)[0] == A.CFD_SUCCESS
+    eo_u, eo_v = cases.tg3_l2_errors(go, fo, 100 * 1e-3)
+    assert eu == pytest.approx(eo_u, rel=1e-9) and ev == pytest.approx(eo_v, rel=1e-9)
+    assert eu < 0.25 and ev < 0.25
