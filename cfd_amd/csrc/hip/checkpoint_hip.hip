@@ -386,12 +386,14 @@ cfd_status_t hip_proj_checkpoint_read(hip_proj_ctx_t* c, const char* path, grid*
     file.fp = nullptr;
     if (r.st == CFD_SUCCESS && !c->T && dalloc(c, &c->T, field_elems(c)) != CFD_SUCCESS)
         r.st = CFD_ERROR_NOMEM;
+    // the file's density may be non-uniform: keep it per cell (RK4 reads rho[idx])
+    if (r.st == CFD_SUCCESS && !c->rho && dalloc(c, &c->rho, field_elems(c)) != CFD_SUCCESS)
+        r.st = CFD_ERROR_NOMEM;
     if (r.st == CFD_SUCCESS) {
         // verified: the scratch copies become the state
         const size_t bytes = field_elems(c) * sizeof(double);
         double* state[CHK_NFIELDS] = {c->u, c->v, c->w, c->p, c->rho, c->T};
         for (int q = 0; q < CHK_NFIELDS && r.st == CFD_SUCCESS; ++q) {
-            if (!state[q]) continue;  // no per-cell density: rho0 only
             if (hipMemcpyAsync(state[q], dst[q], bytes, hipMemcpyDeviceToDevice, c->stream) !=
                 hipSuccess)
                 r.st = CFD_ERROR;

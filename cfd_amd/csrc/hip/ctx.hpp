@@ -82,6 +82,10 @@ struct hip_proj_ctx {
     double *r = nullptr, *pa = nullptr, *pb = nullptr;  // r; CG search directions
     double *pc4 = nullptr, *pd4 = nullptr;               // (ring of CG_XFOLD = 4: pa pb pc4 pd4)
     double *rhs = nullptr, *xt = nullptr;
+    // RK4 borrows r, p_a, p_b, x_tmp as stage buffers and leaves wall values in
+    // them; the CG needs zero wall cells in r and the p ring (lagged-BC
+    // semantics), so the next CG solve clears them first.
+    int cg_scratch_dirty = 0;
     double* Tn = nullptr;  // energy equation output (swapped with T)
     double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated
     double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3

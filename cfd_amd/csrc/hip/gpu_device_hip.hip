@@ -368,8 +368,17 @@ cfd_status_t solve_projection_method_gpu(flow_field* field, const grid* g,
     ns_solver_params_t prm = *params;
     prm.source_amplitude_u = 0.0;  // kernel_predictor has no source term (:98-155)
     prm.source_amplitude_v = 0.0;
-    cfd_status_t s = hip_proj_step_iter_internal(ctx->pc, field, g, &prm, nullptr, params->max_iter);
+    cfd_status_t s = CFD_SUCCESS;
+    // gpu_solver_upload zero-fills d_T when the field has none (:491-495), so
+    // buoyancy / energy then act on T = 0 instead of failing
+    if (!field->T && (prm.beta != 0.0 || prm.alpha > 0.0))
+        s = hip_proj_fill_field(ctx->pc, HIP_FIELD_T, 0.0);
+    if (s == CFD_SUCCESS)
+        s = hip_proj_step_iter_internal(ctx->pc, field, g, &prm, nullptr, params->max_iter);
     gpu_solver_destroy(ctx);
+    // the reference has no NaN scan and returns CFD_SUCCESS after its loop
+    // (:762-769); a non-finite field is downloaded here as there
+    if (s == CFD_ERROR_DIVERGED) s = CFD_SUCCESS;
     return s;
 }
 

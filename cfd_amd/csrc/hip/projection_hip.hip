@@ -133,6 +133,11 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     const DirVals dv{};
     const bool D = dist(c);
     double* x = c->pn;
+    if (c->cg_scratch_dirty) {  // after RK4 stages (rk4_hip.hip): walls of r / p ring to 0
+        for (double* f : {c->r, c->pa, c->pb, c->pc4, c->pd4})
+            HIP_TRY(hipMemsetAsync(f, 0, field_elems(c) * sizeof(double), c->stream));
+        c->cg_scratch_dirty = 0;
+    }
     ST_TRY(halo(c, {x}));
     // poisson_solver_apply_bc(x) at solve start (linear_solver_cg.c:320)
     launch_bc(c, x, 0, dv);
@@ -899,6 +904,8 @@ cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
 cfd_status_t hip_proj_set_density(hip_proj_ctx_t* c, double rho0) {
     if (!c) return CFD_ERROR_INVALID;
     c->rho0 = rho0;
+    // a per-cell density array (RK4, restart files) follows the uniform value
+    if (c->rho) return hip_proj_fill_field(c, HIP_FIELD_RHO, rho0);
     return CFD_SUCCESS;
 }
 
@@ -914,6 +921,11 @@ cfd_status_t hip_proj_upload(hip_proj_ctx_t* c, const flow_field* f) {
         if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
     }
     c->rho0 = f->rho ? f->rho[0] : 1.0;
+    if (c->rho) {  // keep an existing per-cell density in step with the field
+        s = f->rho ? hip_proj_set_field(c, HIP_FIELD_RHO, f->rho)
+                   : hip_proj_fill_field(c, HIP_FIELD_RHO, 1.0);
+        if (s != CFD_SUCCESS) return s;
+    }
     return CFD_SUCCESS;
 }
 
@@ -1250,11 +1262,15 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter
         if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
     }
     c->rho0 = f->rho ? f->rho[0] : 1.0;
+    int done = 0;  // steps completed: the reference leaves them applied to field
     for (int it = 0; it < n_steps; ++it) {
         s = step_device_impl(c, g, prm, stats, it);
         if (s != CFD_SUCCESS) break;
+        ++done;
     }
-    if (s == CFD_SUCCESS || s == CFD_ERROR_DIVERGED) {
+    // a failed step (pressure solve unconverged, communication) leaves the
+    // device u, v, w, p as the completed steps made them
+    if (s == CFD_SUCCESS || s == CFD_ERROR_DIVERGED || done > 0) {
         cfd_status_t d = hip_proj_download(c, f);
         if (d != CFD_SUCCESS) return d;
         if (prm->alpha > 0.0 && f->T && c->T) {

@@ -110,6 +110,7 @@ static cfd_status_t rk4_step_impl(hip_proj_ctx* c, const grid* g, const ns_solve
         launch_stage<3>(c, buoy, rc, a, q0, acc, q0);
     });
     HIP_TRY(hipGetLastError());
+    c->cg_scratch_dirty = 1;  // r, p_a, p_b now hold stage values at the walls
 
     hipLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->red);
     if (energy) ST_TRY(ctx_energy_step(c, g, prm, false));  // solver_rk4.c:213-221

@@ -346,10 +346,19 @@ ns_solver_registry_t* cfd_registry_create(void) {
 
 void cfd_registry_destroy(ns_solver_registry_t* r) { free(r); }
 
-/* name suffix -> backend (solver_registry.c:257-279); `_hip` is a GPU backend */
+/* Name suffix -> backend, as the UNPATCHED reference infers it
+ * (infer_backend_from_type, solver_registry.c:257-279): only `_gpu` is a GPU
+ * name, so `projection_hip` is stored as SCALAR. The one-line patch
+ * INTEGRATION.md §1 asks a maintainer to add (a `_hip` clause at :262-265) is
+ * switched on with cfd_host_set_hip_patch(1). */
+static int g_hip_patch = 0;
+
+void cfd_host_set_hip_patch(int enable) { g_hip_patch = enable ? 1 : 0; }
+
 static ns_solver_backend_t infer_backend(const char* name) {
     if (!name) return NS_SOLVER_BACKEND_SCALAR;
-    if (strstr(name, "_gpu") || strstr(name, "_hip")) return NS_SOLVER_BACKEND_CUDA;
+    if (strstr(name, "_gpu")) return NS_SOLVER_BACKEND_CUDA;
+    if (g_hip_patch && strstr(name, "_hip")) return NS_SOLVER_BACKEND_CUDA;
     if (strstr(name, "_omp")) return NS_SOLVER_BACKEND_OMP;
     if (strstr(name, "_optimized")) return NS_SOLVER_BACKEND_SIMD;
     return NS_SOLVER_BACKEND_SCALAR;
@@ -483,23 +492,80 @@ cfd_status_t solver_solve(ns_solver_t* s, flow_field* f, const grid* g,
     return status;
 }
 
+/* solver_registry.c:1600-1621: the GPU backend asks gpu_is_available(), which
+ * libcfd_hip.so exports (gpu_device_hip.hip); this mirror has no SIMD / OpenMP
+ * solvers of its own. */
 int cfd_backend_is_available(ns_solver_backend_t b) {
     if (b == NS_SOLVER_BACKEND_SCALAR) return 1;
     if (b == NS_SOLVER_BACKEND_CUDA) {
-        int (*avail)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "hip_projection_available");
+        int (*avail)(void) = (int (*)(void))dlsym(RTLD_DEFAULT, "gpu_is_available");
         return avail ? avail() : 0;
     }
     return 0;
 }
 
-const char* cfd_backend_get_name(ns_solver_backend_t b) {
+const char* cfd_backend_get_name(ns_solver_backend_t b) {  /* :1623-1636 */
     switch (b) {
         case NS_SOLVER_BACKEND_SCALAR: return "scalar";
         case NS_SOLVER_BACKEND_SIMD: return "simd";
-        case NS_SOLVER_BACKEND_OMP: return "omp";
-        case NS_SOLVER_BACKEND_CUDA: return "gpu";
+        case NS_SOLVER_BACKEND_OMP: return "openmp";
+        case NS_SOLVER_BACKEND_CUDA: return "cuda";
         default: return "unknown";
     }
+}
+
+/* :1638-1667, on the backend stored at registration */
+int cfd_registry_list_by_backend(ns_solver_registry_t* r, ns_solver_backend_t backend,
+                                 const char** names, int max_count) {
+    if (!r) return 0;
+    int count = 0;
+    for (int i = 0; i < r->count; i++) {
+        if (r->entries[i].backend != backend) continue;
+        if (!names) {
+            count++;
+        } else if (count < max_count) {
+            names[count++] = r->entries[i].name;
+        } else {
+            break;
+        }
+    }
+    return count;
+}
+
+/* :1669-1694: the backend the NAME implies must be available first */
+ns_solver_t* cfd_solver_create_checked(ns_solver_registry_t* r, const char* name) {
+    if (!r || !name) {
+        cfd_set_error(CFD_ERROR_INVALID, "Invalid arguments for solver creation");
+        return NULL;
+    }
+    ns_solver_backend_t b = infer_backend(name);
+    if (!cfd_backend_is_available(b)) {
+        char msg[128];
+        snprintf(msg, sizeof(msg), "Backend '%s' is not available on this system",
+                 cfd_backend_get_name(b));
+        cfd_set_error(CFD_ERROR_UNSUPPORTED, msg);
+        return NULL;
+    }
+    return cfd_solver_create(r, name);
+}
+
+/* simulation_api.c:452-478: a STATIC name table, not the registry. The
+ * reference's own names (CFD_ENABLE_OPENMP build); the HIP names appear only
+ * with the INTEGRATION.md §1 patch, mirrored by the same switch. */
+static const char* const s_solver_names[] = {
+    "explicit_euler", "explicit_euler_optimized", "projection", "projection_optimized",
+    "explicit_euler_gpu", "projection_gpu", "explicit_euler_omp", "projection_omp",
+    "projection_hip", "projection_hip_rbsor", "projection_hip_jacobi", "rk4_hip",
+};
+
+int simulation_list_solvers(const char** names, int max_count) {
+    const int total = (int)(sizeof(s_solver_names) / sizeof(s_solver_names[0]));
+    const int n = g_hip_patch ? total : total - 4;
+    if (names && max_count > 0) {
+        int fill = n < max_count ? n : max_count;
+        for (int i = 0; i < fill; i++) names[i] = s_solver_names[i];
+    }
+    return n;
 }
 
 /* ------------------------------------------------------------------------ */

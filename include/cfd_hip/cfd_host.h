@@ -87,6 +87,20 @@ CFD_HIP_EXPORT cfd_status_t solver_solve(ns_solver_t* solver, flow_field* field,
                                          ns_solver_stats_t* stats);
 CFD_HIP_EXPORT int cfd_backend_is_available(ns_solver_backend_t backend);
 CFD_HIP_EXPORT const char* cfd_backend_get_name(ns_solver_backend_t backend);
+/* solver_registry.c:1638-1694: filter by the backend inferred from the name at
+ * registration; create only when that backend is available */
+CFD_HIP_EXPORT int cfd_registry_list_by_backend(ns_solver_registry_t* registry,
+                                                ns_solver_backend_t backend, const char** names,
+                                                int max_count);
+CFD_HIP_EXPORT ns_solver_t* cfd_solver_create_checked(ns_solver_registry_t* registry,
+                                                      const char* type_name);
+/* Mirror-only switch (no reference counterpart). 0 (default): the registry
+ * behaves like the UNPATCHED reference, whose infer_backend_from_type
+ * (solver_registry.c:257-279) knows only `_gpu`, so `projection_hip` is a
+ * SCALAR entry, and whose simulation_list_solvers table
+ * (simulation_api.c:454-465) lacks the HIP names. 1: the reference with the
+ * INTEGRATION.md §1 edits applied (`_hip` -> GPU backend, HIP names listed). */
+CFD_HIP_EXPORT void cfd_host_set_hip_patch(int enable);
 
 /* simulation API subset (simulation_api.h) */
 typedef struct {
@@ -111,6 +125,8 @@ CFD_HIP_EXPORT void free_simulation(simulation_data* sim);
 CFD_HIP_EXPORT cfd_status_t run_simulation_step(simulation_data* sim);
 CFD_HIP_EXPORT cfd_status_t run_simulation_solve(simulation_data* sim);
 CFD_HIP_EXPORT const ns_solver_stats_t* simulation_get_stats(const simulation_data* sim);
+/* simulation_api.c:452-478: the static name table (see cfd_host_set_hip_patch) */
+CFD_HIP_EXPORT int simulation_list_solvers(const char** names, int max_count);
 
 /* restart files (lib/include/cfd/io/checkpoint.h:49-115, simulation_api.h:93-111):
  * the reference's `.cfdchk` format, status codes and ownership rules */
