@@ -187,6 +187,10 @@ POISSON_METHOD_REDBLACK_SOR = 3
 POISSON_METHOD_CG = 4
 POISSON_METHOD_BICGSTAB = 5
 POISSON_METHOD_MULTIGRID = 6
+NS_SOLVER_BACKEND_SCALAR = 0  # ns_solver_backend_t (navier_stokes_solver.h:172-177)
+NS_SOLVER_BACKEND_SIMD = 1
+NS_SOLVER_BACKEND_OMP = 2
+NS_SOLVER_BACKEND_CUDA = 3
 POISSON_BACKEND_AUTO = 0
 POISSON_BACKEND_SCALAR = 1
 POISSON_BACKEND_OMP = 2

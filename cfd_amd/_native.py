@@ -88,6 +88,12 @@ def _bind_host(lib) -> None:
     _sig(lib, "solver_solve", C.c_int, P(A.NSSolver), P(A.FlowField), P(A.Grid),
          P(A.SolverParams), P(A.SolverStats))
     _sig(lib, "cfd_backend_is_available", C.c_int, C.c_int)
+    _sig(lib, "cfd_backend_get_name", C.c_char_p, C.c_int)
+    _sig(lib, "cfd_registry_list_by_backend", C.c_int, C.c_void_p, C.c_int, P(C.c_char_p),
+         C.c_int)
+    _sig(lib, "cfd_solver_create_checked", P(A.NSSolver), C.c_void_p, C.c_char_p)
+    _sig(lib, "cfd_host_set_hip_patch", None, C.c_int)
+    _sig(lib, "simulation_list_solvers", C.c_int, P(C.c_char_p), C.c_int)
     _sig(lib, "init_simulation_with_solver", P(A.SimulationData), C.c_size_t, C.c_size_t,
          C.c_size_t, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
          C.c_char_p)

@@ -382,6 +382,21 @@ cfd_status_t solve_projection_method_gpu(flow_field* field, const grid* g,
     return s;
 }
 
+static cfd_status_t not_on_path(const char* what) {
+    set_err(CFD_ERROR_UNSUPPORTED, what);
+    return CFD_ERROR_UNSUPPORTED;
+}
+
+cfd_status_t solve_explicit_euler_method_gpu(flow_field*, const grid*, const ns_solver_params_t*,
+                                             const gpu_config_t*) {
+    return not_on_path("GPU explicit Euler solver: not provided by the MI355X projection library");
+}
+
+cfd_status_t solve_rk2_method_gpu(flow_field*, const grid*, const ns_solver_params_t*,
+                                  const gpu_config_t*) {
+    return not_on_path("GPU RK2 solver: not provided by the MI355X projection library");
+}
+
 cfd_status_t solve_rk4_method_gpu(flow_field* field, const grid* g,
                                   const ns_solver_params_t* params, const gpu_config_t* config) {
     // solver_rk_gpu.cu:260-553 (order 4): params->max_iter RK4 steps

@@ -110,6 +110,17 @@ CFD_HIP_EXPORT cfd_status_t solve_projection_method_gpu(flow_field* field, const
 CFD_HIP_EXPORT cfd_status_t solve_rk4_method_gpu(flow_field* field, const grid* grid,
                                                  const ns_solver_params_t* params,
                                                  const gpu_config_t* config);
+/* solver_rk_gpu.cu:535-545 integrators outside the projection path: they
+ * return CFD_ERROR_UNSUPPORTED. Exported so that libcfd_hip.so defines every
+ * symbol of the reference's no-CUDA stub (solver_gpu_stub.c:15-161): a link
+ * that names libcfd_hip.so before libcfd_core.a then never pulls the stub's
+ * object in. */
+CFD_HIP_EXPORT cfd_status_t solve_explicit_euler_method_gpu(flow_field* field, const grid* grid,
+                                                            const ns_solver_params_t* params,
+                                                            const gpu_config_t* config);
+CFD_HIP_EXPORT cfd_status_t solve_rk2_method_gpu(flow_field* field, const grid* grid,
+                                                 const ns_solver_params_t* params,
+                                                 const gpu_config_t* config);
 
 #ifdef __cplusplus
 }
