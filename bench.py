@@ -31,15 +31,6 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# rocprofv3 PMC summary of this workload (tools/gpu_profile.sh + prof_summary.py):
-# 2*FETCH_SIZE + WRITE_SIZE per working launch of sweep A, the gfx950
-# correction of MI355X_MICROARCH.md "HBM [CDNA4]".
-# Newest first; the first file that holds the kernel being reported is used.
-TRAFFIC_JSONS = [ROOT / "profiles" / "r01h_traffic_cg_sweeps.json",
-                 ROOT / "profiles" / "r01g_traffic_cg_sweeps.json",
-                 ROOT / "profiles" / "r01f_traffic_cg_sweeps.json",
-                 ROOT / "profiles" / "r01e_traffic_cg_sweeps.json",
-                 ROOT / "profiles" / "r01c_traffic_cg_sweeps.json"]
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
 BYTES_SWEEP_B = 24.0    # non-fold iterations: read p, r; write r
@@ -63,6 +54,8 @@ def parse():
                     help="CG iterations timed in the CPU baseline sample")
     ap.add_argument("--cpu-scalar-cg-iters", type=int, default=5,
                     help="CG iterations in the 1-thread CPU sample (0: skip it)")
+    ap.add_argument("--cpu-timeout", type=int, default=420,
+                    help="seconds allowed for the CPU baseline child process")
     ap.add_argument("--kchunk", type=int, default=0)
     ap.add_argument("--sweep-rows", type=int, default=16)
     ap.add_argument("--sweep-variant", type=int, default=15,
@@ -175,18 +168,21 @@ def main():
     # cells per step whatever the rank count
     mlups = n_int * args.steps / elapsed / 1e6
     k_mean = sum(iters) / len(iters)
-    step_bytes = (BYTES_STEP_FIXED_SURVEY + BYTES_CG_ITER_SURVEY * k_mean) * n_int
-    gbps_step = step_bytes * args.steps / elapsed / 1e9
+    # SURVEY.md §8d credit: (176 + 80 k) B/cell per step (textbook CG moves 80 B
+    # per iteration; ours moves 58, so this figure can exceed what HBM carried)
+    credited = (BYTES_STEP_FIXED_SURVEY + BYTES_CG_ITER_SURVEY * k_mean) * n_int
+    credited_gbps = credited * args.steps / elapsed / 1e9
 
     kt = ctx.timing()
-    sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s)
+    dflag = "true" if world > 1 else "false"
+    sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s, total ms)
     for key, kname, bpc in (
-            ("cg_sweep_a", f"k_cgA<{args.sweep_rows}, false, {'true' if world > 1 else 'false'}, "
-                           f"{args.sweep_variant}>", BYTES_SWEEP_A),
-            ("cg_sweep_b", f"k_cgB<{args.sweep_rows}, {'true' if world > 1 else 'false'}, "
-                           f"{args.sweep_variant}, false>", BYTES_SWEEP_B),
-            ("cg_sweep_bx", f"k_cgB<{args.sweep_rows}, {'true' if world > 1 else 'false'}, "
-                            f"{args.sweep_variant}, true>", BYTES_SWEEP_BX)):
+            ("cg_sweep_a", f"k_cgA<{args.sweep_rows}, false, {dflag}, {args.sweep_variant}>",
+             BYTES_SWEEP_A),
+            ("cg_sweep_b", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, false>",
+             BYTES_SWEEP_B),
+            ("cg_sweep_bx", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, true>",
+             BYTES_SWEEP_BX)):
         ms, cnt = kt[key]
         avg = ms / cnt if cnt else None
         ach = bpc * n_loc / (avg * 1e-3) / 1e9 if cnt else None
@@ -196,11 +192,29 @@ def main():
     nb = sweeps["cg_sweep_b"][3] + sweeps["cg_sweep_bx"][3]
     avg_b = (sweeps["cg_sweep_b"][5] + sweeps["cg_sweep_bx"][5]) / nb if nb else 0.0
     cg_iter_ms = avg_a + avg_b
-    cg_iter_gbps_survey = BYTES_CG_ITER_SURVEY * n_loc / (cg_iter_ms * 1e-3) / 1e9
     # roofline on the dominant sweep (largest total time)
     dom = max(sweeps, key=lambda k: sweeps[k][5])
     kname, bpc_dom, avg_dom, _, ach_dom, _ = sweeps[dom]
-    traffic, traffic_src = pmc_traffic(kname, n_loc) if world == 1 else (None, None)
+    # measured HBM bytes: the committed PMC profile of THESE kernel sources
+    # (2*FETCH_SIZE + WRITE_SIZE per launch) x this run's launch counts
+    prof = pmc_profile(n_loc)
+    traffic = traffic_src = measured_gbps = None
+    measured_from = []
+    if prof is not None:
+        bpl = prof["kernels"].get(kname, {}).get("hbm_bytes_per_launch")
+        traffic = round(bpl) if bpl else None
+        traffic_src = prof["file"] + ": " + kname if bpl else None
+        names = {k: v[0] for k, v in sweeps.items()}
+        tot = 0.0
+        for key, (ms, cnt) in kt.items():
+            if not cnt:
+                continue
+            kn = names.get(key) or TIMER_KERNEL.get(key)
+            rec = prof["kernels"].get(kn) if kn else None
+            if rec and "hbm_bytes_per_launch" in rec:
+                tot += rec["hbm_bytes_per_launch"] * cnt
+                measured_from.append(kn)
+        measured_gbps = round(tot * world / elapsed / 1e9, 1) if measured_from else None
 
     # measured HBM roof of this GPU (same library, 16-B lanes), after the
     # timed region
@@ -208,6 +222,14 @@ def main():
     cg, tr = C.c_double(0.0), C.c_double(0.0)
     if lib.cfd_hip_stream_bench(local, 1 << 27, 5, C.byref(cg), C.byref(tr)) != A.CFD_SUCCESS:
         cg.value = tr.value = 0.0
+
+    ranks = None
+    if world > 1:  # per-rank device times, so the driver's 1 -> N curve can be read
+        mine = {"rank": rank, "planes": ctx.nz_local - 2,
+                "sweep_ms_per_iter": round(cg_iter_ms, 4),
+                "timers_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
@@ -235,10 +257,11 @@ def main():
                        "parallelism": (f"z-slab x{world} (RCCL halo, "
                                        + ("peer-memory" if comm.device_allreduce else "RCCL")
                                        + " dot all-reduce)") if world > 1 else "single GPU"},
-            "achieved_GBps": round(gbps_step, 1),
+            "measured_GBps": measured_gbps,
+            "measured_GBps_kernels": measured_from or None,
+            "credited_GBps_80": round(credited_gbps, 1),
             "cg_iters_per_step": iters,
             "cg_iter_ms": round(cg_iter_ms, 4),
-            "cg_iter_GBps_survey80": round(cg_iter_gbps_survey, 1),
             "roofline": {"bound": "hbm", "kernel": kname,
                          "achieved": round(ach_dom, 1) if ach_dom else None,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -258,6 +281,7 @@ def main():
                               "avg_ms": round(v[2], 4) if v[2] else None,
                               "achieved_GBps": round(v[4], 1) if v[4] else None}
                           for k, v in sweeps.items()},
+            "ranks": ranks,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
@@ -268,85 +292,52 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kname, cells):
-    """HBM bytes per launch of kernel `kname` from the committed PMC summary,
-    if it was recorded for this kernel variant and grid size (else None)."""
-    for path in TRAFFIC_JSONS:
+# timer -> kernel symbol in the PMC profile (the CG sweeps are named per variant)
+TIMER_KERNEL = {"predictor": "k_predictor<false>", "corrector": "k_corrector",
+                "cg_setup": "k_cg_setup<true, false, true, false>"}
+
+
+def pmc_profile(cells):
+    """The newest committed PMC profile (profiles/*_traffic*.json, written by
+    tools/prof_summary.py) taken on the current HIP sources and this grid, or
+    None: a profile of other kernel code is never used."""
+    from cfd_amd._native import kernel_source_sha
+
+    sha = kernel_source_sha()
+    for path in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
         try:
             d = json.loads(path.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("cells_per_launch") != float(cells):
-            continue
-        for k, v in d.get("kernels", {}).items():
-            if k == kname and "hbm_bytes_per_launch" in v:
-                return round(v["hbm_bytes_per_launch"]), f"{path.name}: {k}"
-    return None, None
-
-
-def host_cpu_model():
-    """`model name` of /proc/cpuinfo (record the host CPU)."""
-    try:
-        for line in Path("/proc/cpuinfo").read_text().splitlines():
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
+        if d.get("source_sha") == sha and d.get("cells_per_launch") == float(cells):
+            d["file"] = path.name
+            return d
     return None
 
 
 def cpu_baseline(n, args, k_gpu):
     """The oracle (OpenMP port of the reference projection) timed on this host
-    on a bounded sample of the same step: predictor, divergence and corrector in
-    full and `cpu_cg_iters` CG iterations on the same 512^3 cavity state; the
-    step time is those phases + k_gpu x the measured CG iteration time."""
-    import numpy as np
+    on a bounded sample of the same step, in a child process that holds no HIP
+    runtime and whose OpenMP runtime starts with OMP_PROC_BIND=close
+    OMP_PLACES=cores (oracle/cpu_baseline.py). Threads: every CPU of this
+    process's affinity mask, but no more than an OMP_NUM_THREADS the box sets
+    (the GPU pool gives each 1-GPU box a 16-CPU share and sets it to 16)."""
+    import subprocess
 
-    from cfd_amd import _abi as A
-    from cfd_amd import api
-    from oracle import oracle
-
-    try:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    except Exception:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(threads, 64))
-    g = api.Grid(n, n, n, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
-    p = api.validation_params(args.dt, 1.0 / args.re)
-    n_int = (n - 2) ** 3
-
-    def sample(nthreads, cg_iters):
-        oracle.set_threads(nthreads)
-        f = api.FlowField(n, n, n)
-        f.rho[...] = 1.0
-        api.cavity_bc(f, 1.0)
-        oracle.lib().oracle_set_poisson_cap(cg_iters)
-        t0 = time.perf_counter()
-        s, _, it = oracle.projection_step(f, g, p)
-        wall = time.perf_counter() - t0
-        oracle.lib().oracle_set_poisson_cap(0)
-        ph = oracle.last_phase_ms()
-        t_cg_iter = ph[2] / max(it, 1) / 1e3
-        t_step = (ph[0] + ph[1] + ph[3]) / 1e3 + k_gpu * t_cg_iter
-        return s, it, wall, t_cg_iter, t_step
-
-    s, it, wall, t_cg_iter, t_step = sample(threads, args.cpu_cg_iters)
-    out = {"value": round(n_int / t_step / 1e6, 4), "unit": "MLUPS", "cores": threads,
-           "kind": "port",
-           "sample": (f"{n}^3 cavity step 1 on the host: predictor+divergence+corrector timed "
-                      f"in full, {it} CG iterations timed ({t_cg_iter*1e3:.1f} ms/iter) and "
-                      f"scaled to the GPU's {k_gpu:.0f} iterations/step; OpenMP x{threads}; "
-                      f"sample wall {wall:.1f} s"),
-           "cg_iter_ms": round(t_cg_iter * 1e3, 2), "status": s,
-           "host_cpu_model": host_cpu_model(), "host_cpus": os.cpu_count()}
-    if args.cpu_scalar_cg_iters > 0:
-        # the scalar reference configuration (SURVEY.md §8d (i)): one thread
-        s1, it1, wall1, t1_cg, t1_step = sample(1, args.cpu_scalar_cg_iters)
-        out["scalar_1core"] = {"value": round(n_int / t1_step / 1e6, 4), "unit": "MLUPS",
-                               "cores": 1, "cg_iter_ms": round(t1_cg * 1e3, 1),
-                               "sample": f"same step, {it1} CG iterations timed, wall {wall1:.1f} s",
-                               "status": s1}
-    oracle.set_threads(threads)
+    affinity = len(os.sched_getaffinity(0))
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(affinity, env_threads) if env_threads > 0 else affinity
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close",
+               OMP_PLACES="cores", CFD_AMD_NO_TORCH="1")
+    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--size", str(n), "--dt", str(args.dt),
+           "--re", str(args.re), "--k-gpu", str(k_gpu), "--cg-iters", str(args.cpu_cg_iters),
+           "--scalar-cg-iters", str(args.cpu_scalar_cg_iters)]
+    r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
+                       timeout=args.cpu_timeout)
+    if r.returncode != 0:
+        return {"error": f"cpu baseline exit {r.returncode}: {r.stderr.strip()[-400:]}"}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["omp_num_threads_env"] = env_threads or None
     return out
 
 

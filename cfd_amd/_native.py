@@ -39,6 +39,19 @@ def build(force: bool = False, jobs: int = 4) -> None:
     subprocess.run(args, check=True)
 
 
+def kernel_source_sha() -> str:
+    """sha256 over the HIP sources (csrc/hip/*.hip, *.hpp) the built library
+    came from: PMC profiles record it, bench.py uses a profile's byte counts
+    only for the same kernels."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted((CSRC_DIR / "hip").glob("*.hip")) + sorted((CSRC_DIR / "hip").glob("*.hpp")):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def _ensure_built() -> None:
     if HIP_LIB.exists() and HOST_LIB.exists():
         return

@@ -13,10 +13,10 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
     python3 bench.py $ARGS > $OUT/bench_trace.log 2>&1
 rc=$?; echo "trace exit $rc"; [ $rc -ne 0 ] && exit $rc
 if [ -z "${NO_PMC}" ]; then
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_cg[AB]" -d $OUT/fetch -o run --output-format csv -- \
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- \
     python3 bench.py $ARGS > $OUT/bench_fetch.log 2>&1
 rc=$?; echo "fetch exit $rc"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_cg[AB]" -d $OUT/write -o run --output-format csv -- \
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- \
     python3 bench.py $ARGS > $OUT/bench_write.log 2>&1
 rc=$?; echo "write exit $rc"; [ $rc -ne 0 ] && exit $rc
 fi

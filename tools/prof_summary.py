@@ -104,8 +104,11 @@ def main():
                 if cells:
                     rec["hbm_bytes_per_cell"] = rec["hbm_bytes_per_launch"] / cells
             out[k] = rec
+        sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+        from cfd_amd._native import kernel_source_sha
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as fh:
             json.dump({"source": str(d), "correction": "2*FETCH_SIZE + WRITE_SIZE",
+                       "source_sha": kernel_source_sha(),
                        "cells_per_launch": cells, "kernels": out}, fh, indent=1)
 
 
