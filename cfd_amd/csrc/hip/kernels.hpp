@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mbox.hpp"
 
 namespace cfdhip {
@@ -1738,14 +1740,56 @@ static __global__ void k_rx_finish(RxState* st, const unsigned long long* gred, 
 constexpr int RB1_OX = 124;  // output columns per tile (lanes 1..62)
 constexpr int RB1_OY = 12;   // output rows per tile (waves 2..13)
 
-template <int FL>
-static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
+// One SOR update of a cell (linear_solver_redblack.c:103-112 operation order).
+__device__ __forceinline__ double sor1(const RelaxCoef& rc, double vc, double vl, double vr,
+                                       double vs, double vn, double vm, double vp, double vb) {
+    const double pn = -(vb - divc(vr + vl, rc.dx2, rc.rdx2) - divc(vn + vs, rc.dy2, rc.rdy2) -
+                        (vp + vm) * rc.inv_dz2) *
+                      rc.inv_factor;
+    return vc + rc.omega * (pn - vc);
+}
+
+// |lap(x) - rhs| of one cell (linear_solver.c:304-346, the division form).
+__device__ __forceinline__ double res1(const RelaxCoef& rc, double c, double xl, double xr,
+                                       double ys, double yn, double zm, double zp, double b) {
+    const double l = divc(xr - 2.0 * c + xl, rc.dx2, rc.rdx2) +
+                     divc(yn - 2.0 * c + ys, rc.dy2, rc.rdy2) + (zp + zm - 2.0 * c) * rc.inv_dz2;
+    return fabs(l - b);
+}
+
+template <bool V>
+using BoolC = std::integral_constant<bool, V>;
+template <int V>
+using IntC = std::integral_constant<int, V>;
+
+// Issue-model details (r02; profiles/r02_rb_variants.jsonl, r02_pmc_rb.jsonl):
+//  - the colour pattern of a step is wave-uniform ((j + q) parity): the z
+//    loop is unrolled by two planes and each step is compiled for its
+//    pattern, so no per-lane selects pick the updated cell of a pair
+//    (VALU instructions per launch 321 M -> 196 M at 512^3);
+//  - x neighbours come from the row the wave already published in LDS (one
+//    ds_read_b64 each side) instead of two ds_bpermute per double, and every
+//    LDS operand of a step is read right after its barrier (one LDS round
+//    trip per step);
+//  - rhs is not loaded on the two halo rows, which never use it.
+// ROWS > 1 (several rows per wave, fewer waves) and a register plane
+// prefetch (PFQ) are kept as template options: at 512^3 both measured slower
+// (two rows: 190 / 142 VGPRs, one workgroup per CU; prefetch at one row
+// spills), so the product instantiates <FL, 1, false>.
+template <int ROWS>
+constexpr int rb1_threads() { return 64 * 16 / ROWS; }
+template <int ROWS>
+constexpr int rb1_min_waves() { return ROWS == 1 ? 4 : 2; }
+
+template <int FL, int ROWS, bool PFQ>
+static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) void k_rb1(
     SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
     const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
-    constexpr bool PF = (FL & SW_PREFETCH) != 0;
+    constexpr bool PF = PFQ;
+    constexpr int NW = 16 / ROWS;  // waves
     __shared__ double2 xb[2][16][64];  // X rows by plane parity
     __shared__ double2 rb[2][16][64];  // R rows by plane parity
-    __shared__ double sh[16];
+    __shared__ double sh[NW];
     __shared__ int flag;
     if (st->done) return;
     const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
@@ -1754,124 +1798,179 @@ static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
     const int rest = t / g.tiles_x;
     const int ty = rest % g.tiles_y;
     const int tz = rest / g.tiles_y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lm = (lane - 1) & 63, lp = (lane + 1) & 63;  // x neighbours' lanes
     const int i0 = tx * RB1_OX - 2 + 2 * lane;  // even; the pair is (i0, i0 + 1)
-    const int j = ty * RB1_OY - 2 + w;
+    const int r0w = ROWS * w;                   // tile rows r0w .. r0w + ROWS - 1
+    const int j0 = ty * RB1_OY - 2 + r0w;       // grid row of tile row r0w
     const int kb = g.k0 + tz * g.kc;
     const int ke = min(kb + g.kc, g.k1);
-    const bool ld = (j >= 0 && j < g.ny && i0 >= 0 && i0 < g.nx);
-    const bool jin = (j >= 1 && j <= g.ny - 2);
-    const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;
-    const bool in1 = jin && i0 + 1 <= g.nx - 2;  // i0 + 1 >= 1 always
-    const bool ownrow = (w >= 2 && w < 2 + RB1_OY);
-    const bool own = ownrow && (lane >= 1 && lane <= 62);
-    const bool rrow = (w >= 1 && w <= 14);
-    const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
+    const bool xin = (i0 >= 0 && i0 < g.nx);
+    const bool lanes_own = (lane >= 1 && lane <= 62);
+    bool ld[ROWS], jin[ROWS], in0[ROWS], in1[ROWS], own[ROWS], orow[ROWS], rrow[ROWS];
+    long long col[ROWS];
+#pragma unroll
+    for (int s = 0; s < ROWS; ++s) {
+        const int j = j0 + s, r = r0w + s;
+        ld[s] = xin && j >= 0 && j < g.ny;
+        jin[s] = (j >= 1 && j <= g.ny - 2);
+        in0[s] = jin[s] && i0 >= 1 && i0 <= g.nx - 2;
+        in1[s] = jin[s] && i0 + 1 <= g.nx - 2;
+        orow[s] = (r >= 2 && r < 2 + RB1_OY);   // wave-uniform
+        rrow[s] = (r >= 1 && r <= 14);          // wave-uniform
+        own[s] = orow[s] && lanes_own;
+        col[s] = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
+    }
+    auto ldx = [&](int s, int k) -> double2 {
+        return (ld[s] && k >= 0 && k < g.nz) ? ld2(X, (long long)k * g.ps + col[s])
+                                             : make_double2(0.0, 0.0);
+    };
+    auto ldr = [&](int s, int k) -> double2 {  // rows without R work never read rhs
+        return (ld[s] && rrow[s] && k >= 0 && k < g.nz)
+                   ? ld2v<FL>(rhs, (long long)k * g.ps + col[s])
+                   : make_double2(0.0, 0.0);
+    };
     const double2 zero = make_double2(0.0, 0.0);
-    auto ldx = [&](int k) -> double2 {
-        return (ld && k >= 0 && k < g.nz) ? ld2(X, (long long)k * g.ps + col) : make_double2(0.0, 0.0);
-    };
-    auto ldr = [&](int k) -> double2 {
-        return (ld && k >= 0 && k < g.nz) ? ld2v<FL>(rhs, (long long)k * g.ps + col)
-                                          : make_double2(0.0, 0.0);
-    };
-    // step q forms R_{q+1} and updates the second colour of plane q.
-    // Registers: X_q, X_{q+1}, X_{q+2} (xm, xc, xp); R_{q-1}, R_q (rmm, rm);
-    // rhs_{q+1}, rhs_q (bq, bm). LDS at the top of step q: X_{q+1} rows in
-    // xb[(q+1)&1], R_q rows in rb[q&1]; one barrier per plane.
-    int q = kb - 2;
-    double2 xm = ldx(q), xc = ldx(q + 1), xp = ldx(q + 2);
-    double2 bq = ldr(q + 1), bm = zero, rmm = zero, rm = zero;
-    double2 nx_x = PF ? ldx(q + 3) : zero, nx_b = PF ? ldr(q + 2) : zero;
-    xb[(q + 1) & 1][w][lane] = xc;
+    // Step q forms R_{q+1} and updates the second colour of plane q.
+    // Per row: X_q, X_{q+1}, X_{q+2} (xm, xc, xp); R_{q-1}, R_q (rmm, rm);
+    // rhs_{q+1} (bq); prefetched X_{q+3} / rhs_{q+2} (nx, nb). Of rhs_q and
+    // R_{q-1} only the component of the cell this step's second-colour
+    // update touches is kept (bmh, rmmh): the pattern alternates per plane,
+    // so the end of step q keeps the component step q + 1 will use.
+    // LDS at the top of step q: X_{q+1} rows in xb[(q+1)&1], R_q rows in rb[q&1].
+    double2 xm[ROWS], xc[ROWS], xp[ROWS], bq[ROWS], rm[ROWS], nx[ROWS], nb[ROWS];
+    double bmh[ROWS], rmmh[ROWS];
+#pragma unroll
+    for (int s = 0; s < ROWS; ++s) {
+        xm[s] = ldx(s, kb - 2);
+        xc[s] = ldx(s, kb - 1);
+        xp[s] = ldx(s, kb);
+        bq[s] = ldr(s, kb - 1);
+        rm[s] = zero;
+        bmh[s] = rmmh[s] = 0.0;
+        nx[s] = PF ? ldx(s, kb + 1) : zero;
+        nb[s] = PF ? ldr(s, kb) : zero;
+        xb[(kb - 1) & 1][r0w + s][lane] = xc[s];
+    }
     double m = 0.0;
-    for (; q < ke; ++q) {
-        double2 fx = zero, fb = zero;  // X_{q+3}, rhs_{q+2}
-        if (PF) {
-            fx = nx_x;
-            fb = nx_b;
-            if (q + 1 < ke) {
-                nx_x = ldx(q + 4);
-                nx_b = ldr(q + 3);
+    // E: cell i0 of the pair is the cell both updates of this step touch (the
+    // first colour, (i+j+k) odd, of plane q+1 and the second of plane q) in
+    // the wave's first row; its second row has the other pattern
+    auto step = [&](auto Ec, int q) __attribute__((always_inline)) {
+        constexpr bool E = decltype(Ec)::value;
+        double2 fx[ROWS], fb[ROWS];
+#pragma unroll
+        for (int s = 0; s < ROWS; ++s) {
+            fx[s] = nx[s];
+            fb[s] = nb[s];
+            if (PF && q + 1 < ke) {
+                nx[s] = ldx(s, q + 4);
+                nb[s] = ldr(s, q + 3);
             }
         }
         __syncthreads();
         const int qa = q + 1;
-        // ---- R_{q+1} and the residual of X at plane q+1 ----
         const bool qin = (qa >= g.k0 && qa < g.k1);
-        double2 R = xc;
-        if (rrow) {
-            const double2 ys = xb[qa & 1][w - 1][lane];
-            const double2 yn = xb[qa & 1][w + 1][lane];
-            const double left = __shfl_up(xc.y, 1, 64);
-            const double right = __shfl_down(xc.x, 1, 64);
-            const bool first = ((j + qa + g.kofs) & 1) == 1;  // cell i0 has the odd parity
-            const double vc = first ? xc.x : xc.y;
-            const double vl = first ? left : xc.x, vr = first ? xc.y : right;
-            const double vs = first ? ys.x : ys.y, vn = first ? yn.x : yn.y;
-            const double vm = first ? xm.x : xm.y, vp = first ? xp.x : xp.y;
-            const double vb = first ? bq.x : bq.y;
-            if (qin && (first ? in0 : in1)) {
-                const double pn = -(vb - divc(vr + vl, rc.dx2, rc.rdx2) -
-                                    divc(vn + vs, rc.dy2, rc.rdy2) -
-                                    (vp + vm) * rc.inv_dz2) *
-                                  rc.inv_factor;
-                const double xn = vc + rc.omega * (pn - vc);
-                if (first) R.x = xn;
-                else R.y = xn;
+        const bool rin = qin && qa >= kb && qa < ke;
+        // the output's LDS operands (R_q rows) are read up front, so one LDS
+        // round trip after the barrier serves both halves of the step
+        const int wlo = max(r0w - 1, 0), whi = min(r0w + ROWS, 15);
+        const double2 rys = rb[q & 1][wlo][lane];
+        const double2 ryn = rb[q & 1][whi][lane];
+        double rlr[ROWS];
+#pragma unroll
+        for (int s = 0; s < ROWS; ++s) {
+            const bool Es = (s & 1) ? !E : E;
+            rlr[s] = Es ? reinterpret_cast<const double*>(&rb[q & 1][r0w + s][lm])[1]
+                        : reinterpret_cast<const double*>(&rb[q & 1][r0w + s][lp])[0];
+        }
+        double2 R[ROWS];
+        // ---- R_{q+1} and the residual of X at plane q+1 ----
+#pragma unroll
+        for (int s = 0; s < ROWS; ++s) {
+            const bool Es = (s & 1) ? !E : E;
+            // two rows: one at a time (interleaving them raises the register
+            // demand); one row: let the output's LDS reads rise to the top
+            if constexpr (ROWS > 1) __builtin_amdgcn_sched_barrier(0);
+            R[s] = xc[s];
+            const double2 ys = (s == 0) ? xb[qa & 1][wlo][lane] : xc[s > 0 ? s - 1 : 0];
+            const double2 yn = (s == ROWS - 1) ? xb[qa & 1][whi][lane] : xc[s < ROWS - 1 ? s + 1 : s];
+            const double left = reinterpret_cast<const double*>(&xb[qa & 1][r0w + s][lm])[1];
+            const double right = reinterpret_cast<const double*>(&xb[qa & 1][r0w + s][lp])[0];
+            if (!rrow[s] || !qin) continue;
+            if (Es) {
+                const double v = sor1(rc, xc[s].x, left, xc[s].y, ys.x, yn.x, xm[s].x, xp[s].x,
+                                      bq[s].x);
+                if (in0[s]) R[s].x = v;
+            } else {
+                const double v = sor1(rc, xc[s].y, xc[s].x, right, ys.y, yn.y, xm[s].y, xp[s].y,
+                                      bq[s].y);
+                if (in1[s]) R[s].y = v;
             }
-            if (own && qin && qa >= kb && qa < ke) {
-                const double l0 = divc(xc.y - 2.0 * xc.x + left, rc.dx2, rc.rdx2) +
-                                  divc(yn.x - 2.0 * xc.x + ys.x, rc.dy2, rc.rdy2) +
-                                  (xp.x + xm.x - 2.0 * xc.x) * rc.inv_dz2;
-                const double l1 = divc(right - 2.0 * xc.y + xc.x, rc.dx2, rc.rdx2) +
-                                  divc(yn.y - 2.0 * xc.y + ys.y, rc.dy2, rc.rdy2) +
-                                  (xp.y + xm.y - 2.0 * xc.y) * rc.inv_dz2;
-                const double r0 = fabs(l0 - bq.x), r1 = fabs(l1 - bq.y);
-                if (in0 && r0 > m) m = r0;
-                if (in1 && r1 > m) m = r1;
+            if (orow[s] && rin) {
+                const double a0 = res1(rc, xc[s].x, left, xc[s].y, ys.x, yn.x, xm[s].x, xp[s].x,
+                                       bq[s].x);
+                const double a1 = res1(rc, xc[s].y, xc[s].x, right, ys.y, yn.y, xm[s].y,
+                                       xp[s].y, bq[s].y);
+                if (own[s] && in0[s] && a0 > m) m = a0;
+                if (own[s] && in1[s] && a1 > m) m = a1;
             }
         }
         // ---- second colour of plane q from R_{q-1}, R_q, R_{q+1} ----
-        if (q >= kb && ownrow) {  // wave-uniform: shuffles below
-            const double2 ys = rb[q & 1][w - 1][lane];
-            const double2 yn = rb[q & 1][w + 1][lane];
-            const double left = __shfl_up(rm.y, 1, 64);
-            const double right = __shfl_down(rm.x, 1, 64);
-            const bool first = ((j + q + g.kofs) & 1) == 0;  // cell i0 has the even parity
-            const double vc = first ? rm.x : rm.y;
-            const double vl = first ? left : rm.x, vr = first ? rm.y : right;
-            const double vs = first ? ys.x : ys.y, vn = first ? yn.x : yn.y;
-            const double vm = first ? rmm.x : rmm.y, vp = first ? R.x : R.y;
-            const double vb = first ? bm.x : bm.y;
-            double2 out = rm;
-            if (own && (first ? in0 : in1)) {
-                const double pn = -(vb - divc(vr + vl, rc.dx2, rc.rdx2) -
-                                    divc(vn + vs, rc.dy2, rc.rdy2) -
-                                    (vp + vm) * rc.inv_dz2) *
-                                  rc.inv_factor;
-                const double xn = vc + rc.omega * (pn - vc);
-                if (first) out.x = xn;
-                else out.y = xn;
+        if (q >= kb) {
+#pragma unroll
+            for (int s = 0; s < ROWS; ++s) {
+                const bool Es = (s & 1) ? !E : E;
+                if constexpr (ROWS > 1) __builtin_amdgcn_sched_barrier(0);
+                if (!orow[s]) continue;
+                const double2 ys = (s == 0) ? rys : rm[s > 0 ? s - 1 : 0];
+                const double2 yn = (s == ROWS - 1) ? ryn : rm[s < ROWS - 1 ? s + 1 : s];
+                double2 out = rm[s];
+                if (Es) {
+                    const double v = sor1(rc, rm[s].x, rlr[s], rm[s].y, ys.x, yn.x, rmmh[s],
+                                          R[s].x, bmh[s]);
+                    if (own[s] && in0[s]) out.x = v;
+                } else {
+                    const double v = sor1(rc, rm[s].y, rm[s].x, rlr[s], ys.y, yn.y, rmmh[s],
+                                          R[s].y, bmh[s]);
+                    if (own[s] && in1[s]) out.y = v;
+                }
+                if (own[s] && ld[s] && jin[s]) st2v<FL>(Y, (long long)q * g.ps + col[s], out);
             }
-            if (own && ld && jin) st2v<FL>(Y, (long long)q * g.ps + col, out);
         }
-        rmm = rm;
-        rm = R;
-        bm = bq;
-        xm = xc;
-        xc = xp;
-        if (PF) {
-            xp = fx;
-            bq = fb;
-        } else {
-            xp = ldx(q + 3);
-            bq = ldr(q + 2);
+#pragma unroll
+        for (int s = 0; s < ROWS; ++s) {
+            // step q + 1 updates the .x cell of this row iff this step did not
+            const bool En = (s & 1) ? E : !E;
+            rmmh[s] = En ? rm[s].x : rm[s].y;
+            rm[s] = R[s];
+            bmh[s] = En ? bq[s].x : bq[s].y;
+            xm[s] = xc[s];
+            xc[s] = xp[s];
+            xp[s] = PF ? fx[s] : ldx(s, q + 3);
+            bq[s] = PF ? fb[s] : ldr(s, q + 2);
+            // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were
+            // last read in step q - 1, before this step's barrier)
+            xb[(q + 2) & 1][r0w + s][lane] = xc[s];
+            rb[(q + 1) & 1][r0w + s][lane] = rm[s];
         }
-        // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were last
-        // read in step q - 1, before this step's barrier)
-        xb[(q + 2) & 1][w][lane] = xc;
-        rb[(q + 1) & 1][w][lane] = rm;
+    };
+    // E(q) for the wave's first row: ((j0 + q + kofs) & 1) == 0; E(kb - 2) == E(kb)
+    const bool E0 = __builtin_amdgcn_readfirstlane(((j0 + kb + g.kofs) & 1) == 0 ? 1 : 0) != 0;
+    int q = kb - 2;
+    if (E0) {
+        for (; q + 1 < ke; q += 2) {
+            step(BoolC<true>{}, q);
+            step(BoolC<false>{}, q + 1);
+        }
+        if (q < ke) step(BoolC<true>{}, q);
+    } else {
+        for (; q + 1 < ke; q += 2) {
+            step(BoolC<false>{}, q);
+            step(BoolC<true>{}, q + 1);
+        }
+        if (q < ke) step(BoolC<false>{}, q);
     }
     m = wave_max(m);
     if (lane == 0) sh[w] = m;
@@ -1879,7 +1978,7 @@ static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
     double* shs = (double*)&xb[0][0][0];
     if (threadIdx.x == 0) {
         double a = 0.0;
-        for (int v = 0; v < 16; ++v) a = fmax(a, sh[v]);
+        for (int v = 0; v < NW; ++v) a = fmax(a, sh[v]);
         store_sc1(&partials[blockIdx.x], a);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned tk = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
@@ -1889,13 +1988,14 @@ static __global__ __launch_bounds__(1024, sweep_min_waves<FL>()) void k_rb1(
     __syncthreads();
     if (flag == 0) return;
     double a = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += 1024) a = fmax(a, load_sc1(&partials[b]));
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += rb1_threads<ROWS>())
+        a = fmax(a, load_sc1(&partials[b]));
     a = wave_max(a);
     if (lane == 0) shs[w] = a;
     __syncthreads();
     if (threadIdx.x == 0) {
         double tot = 0.0;
-        for (int v = 0; v < 16; ++v) tot = fmax(tot, shs[v]);
+        for (int v = 0; v < NW; ++v) tot = fmax(tot, shs[v]);
         __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rx_finish(st, tot, it);
     }

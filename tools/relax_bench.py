@@ -19,15 +19,19 @@ from cfd_amd import api  # noqa: E402
 
 def main():
     n = int(os.environ.get("N", "512"))
+    nx, ny, nz = (int(os.environ.get(k, str(n))) for k in ("NX", "NY", "NZ"))
     iters = int(os.environ.get("ITERS", "40"))
-    rhs = np.zeros((n, n, n))
-    rhs[1:-1, 1:-1, 1:-1] = np.cos(np.linspace(0, 3, n - 2))[None, None, :]
+    methods = os.environ.get("METHODS", "rbsor,jacobi").split(",")
+    rhs = np.zeros((nz, ny, nx))
+    rhs[1:-1, 1:-1, 1:-1] = np.cos(np.linspace(0, 3, nx - 2))[None, None, :]
     rhs -= rhs[1:-1, 1:-1, 1:-1].mean() * (rhs != 0)
-    d = 1.0 / (n - 1)
-    cells = (n - 2) ** 3
+    d = 1.0 / (nx - 1)
+    cells = (nx - 2) * (ny - 2) * (nz - 2)
     for name, method in (("rbsor", A.HIP_POISSON_REDBLACK), ("jacobi", A.HIP_POISSON_JACOBI)):
-        ctx = api.HipProjection(n, n, n)
-        x = np.zeros((n, n, n))
+        if name not in methods:
+            continue
+        ctx = api.HipProjection(nx, ny, nz)
+        x = np.zeros((nz, ny, nx))
         prm = A.PoissonParams(0.0, 0.0, 3, 0.0, 1, False, 0)
         ctx.poisson_solve(method, x, rhs, d, d, d, prm)   # warm-up
         prm = A.PoissonParams(0.0, 0.0, iters, 0.0, 1, False, 0)
@@ -41,7 +45,8 @@ def main():
         ctx.close()
         relax, res = kt["relax"], kt["residual"]
         per_it = (relax[0] + res[0]) / iters
-        print(json.dumps({"method": name, "n": n, "iters": st.iterations, "status": s,
+        print(json.dumps({"method": name, "grid": [nx, ny, nz], "iters": st.iterations, "status": s,
+                          "rb_variant": os.environ.get("CFD_HIP_RB_VARIANT"),
                           "iter_ms_kernels": round(per_it, 4),
                           "relax_ms": round(relax[0] / iters, 4),
                           "residual_ms": round(res[0] / max(res[1], 1), 4),
