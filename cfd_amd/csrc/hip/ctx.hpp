@@ -61,6 +61,7 @@ struct hip_proj_ctx {
     SGeo sgeo{};       // row-pair CG sweep tiling
     SGeo sg_edge{}, sg_int{};  // slabs: sweep B split into edge planes + interior
     SGeo rgeo{};               // single-pass RB-SOR tiling (k_rb1)
+    SGeo pgeo{};               // predictor / corrector z-march tiling (k_pred2, k_corr2)
     int split_b = 0;
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup
     int sweep_variant = 0;  // SW_NT_* flags of the CG sweeps

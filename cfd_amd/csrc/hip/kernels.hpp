@@ -900,171 +900,6 @@ static __global__ __launch_bounds__(256) void k_bc_shell(Geo g, double* __restri
     }
 }
 
-// ---------------------------------------------------------------------------
-// Predictor (solver_projection.c:116-185) fused with the boundary copy
-// (boundary_copy_utils.h:93-148): interior cells get
-//   u* = clamp(u + dt((-(u.grad)u + nu lap u) + s)),
-// boundary cells get u* = u (u_star starts as a copy of u and its faces are
-// then restored from u, so the boundary of u* is always u's).
-// Source term s: per-row / per-column tables computed on the host with the
-// reference's libm expression (compute_source_terms at iter = 0), plus
-// Boussinesq buoyancy (energy_solver.c:185-196) when beta != 0.
-// ---------------------------------------------------------------------------
-struct PredCoef {
-    double two_dx, two_dy, inv_2dz;   // first derivatives
-    double dx_sq, dy_sq, inv_dz2;     // second derivatives
-    double dt, nu;
-    double beta, T_ref, g0, g1, g2;
-};
-
-template <bool BUOY>
-static __global__ __launch_bounds__(256) void k_predictor(Geo g, PredCoef pc,
-                                                   const double* __restrict__ U,
-                                                   const double* __restrict__ V,
-                                                   const double* __restrict__ W,
-                                                   const double* __restrict__ T,
-                                                   const double* __restrict__ src_u_row,
-                                                   const double* __restrict__ src_v_col,
-                                                   double* __restrict__ us,
-                                                   double* __restrict__ vs,
-                                                   double* __restrict__ ws) {
-    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int k = blockIdx.z;
-    if (i >= g.nx || j >= g.ny) return;
-    const long long idx = cidx(g, i, j, k);
-    const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
-                           k >= g.k0 && k < g.k1);
-    if (!interior) {
-        us[idx] = U[idx];
-        vs[idx] = V[idx];
-        ws[idx] = W[idx];
-        return;
-    }
-    const long long px = g.px, sz = g.sz;
-    double u = U[idx], v = V[idx], w = W[idx];
-    double du_dx = (U[idx + 1] - U[idx - 1]) / pc.two_dx;
-    double du_dy = (U[idx + px] - U[idx - px]) / pc.two_dy;
-    double du_dz = (U[idx + sz] - U[idx - sz]) * pc.inv_2dz;
-    double dv_dx = (V[idx + 1] - V[idx - 1]) / pc.two_dx;
-    double dv_dy = (V[idx + px] - V[idx - px]) / pc.two_dy;
-    double dv_dz = (V[idx + sz] - V[idx - sz]) * pc.inv_2dz;
-    double dw_dx = (W[idx + 1] - W[idx - 1]) / pc.two_dx;
-    double dw_dy = (W[idx + px] - W[idx - px]) / pc.two_dy;
-    double dw_dz = (W[idx + sz] - W[idx - sz]) * pc.inv_2dz;
-    double conv_u = u * du_dx + v * du_dy + w * du_dz;
-    double conv_v = u * dv_dx + v * dv_dy + w * dv_dz;
-    double conv_w = u * dw_dx + v * dw_dy + w * dw_dz;
-    double d2u_dx2 = (U[idx + 1] - 2.0 * u + U[idx - 1]) / pc.dx_sq;
-    double d2u_dy2 = (U[idx + px] - 2.0 * u + U[idx - px]) / pc.dy_sq;
-    double d2u_dz2 = (U[idx + sz] - 2.0 * u + U[idx - sz]) * pc.inv_dz2;
-    double d2v_dx2 = (V[idx + 1] - 2.0 * v + V[idx - 1]) / pc.dx_sq;
-    double d2v_dy2 = (V[idx + px] - 2.0 * v + V[idx - px]) / pc.dy_sq;
-    double d2v_dz2 = (V[idx + sz] - 2.0 * v + V[idx - sz]) * pc.inv_dz2;
-    double d2w_dx2 = (W[idx + 1] - 2.0 * w + W[idx - 1]) / pc.dx_sq;
-    double d2w_dy2 = (W[idx + px] - 2.0 * w + W[idx - px]) / pc.dy_sq;
-    double d2w_dz2 = (W[idx + sz] - 2.0 * w + W[idx - sz]) * pc.inv_dz2;
-    double visc_u = pc.nu * (d2u_dx2 + d2u_dy2 + d2u_dz2);
-    double visc_v = pc.nu * (d2v_dx2 + d2v_dy2 + d2v_dz2);
-    double visc_w = pc.nu * (d2w_dx2 + d2w_dy2 + d2w_dz2);
-    double su = src_u_row[j];
-    double sv = src_v_col[i];
-    double sw = 0.0;
-    if (BUOY) {
-        double dT = T[idx] - pc.T_ref;
-        su += -pc.beta * dT * pc.g0;
-        sv += -pc.beta * dT * pc.g1;
-        sw += -pc.beta * dT * pc.g2;
-    }
-    double a = u + pc.dt * (-conv_u + visc_u + su);
-    double b = v + pc.dt * (-conv_v + visc_v + sv);
-    double c = w + pc.dt * (-conv_w + visc_w + sw);
-    us[idx] = fmax(-100.0, fmin(100.0, a));
-    vs[idx] = fmax(-100.0, fmin(100.0, b));
-    ws[idx] = fmax(-100.0, fmin(100.0, c));
-}
-
-// ---------------------------------------------------------------------------
-// Corrector (solver_projection.c:230-250) + boundary restore (:277-278) +
-// NaN/Inf scan (:281-289) + stats (solver_registry.c:31-49), one pass.
-// Interior: u = clamp(u* - (dt/rho) grad p). Boundary cells keep u (== u*).
-// Every cell contributes to max |u| and max |p| and the non-finite flag.
-// red[0] = encoded max velocity, red[1] = encoded max |p|, red[2] = nonfinite.
-// ---------------------------------------------------------------------------
-struct CorrCoef {
-    double two_dx, two_dy, inv_2dz;
-    double dt_over_rho;
-};
-constexpr int CORR_KC = 64;  // planes per corrector workgroup
-
-static __global__ __launch_bounds__(256) void k_corrector(Geo g, CorrCoef cc,
-                                                   const double* __restrict__ us,
-                                                   const double* __restrict__ vs,
-                                                   const double* __restrict__ ws,
-                                                   const double* __restrict__ P,
-                                                   double* __restrict__ U, double* __restrict__ V,
-                                                   double* __restrict__ W,
-                                                   unsigned long long* red) {
-    __shared__ double shv[4], shp[4];
-    __shared__ int shbad;
-    if (threadIdx.x == 0) shbad = 0;
-    __syncthreads();
-    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-    // each workgroup walks a chunk of planes: few workgroups -> few atomics.
-    // Planes [ks, ke): the owned planes plus the global z faces; a Z-slab's
-    // halo planes belong to the neighbour and are left out of the maxima.
-    const int ks = (g.nz > 1 && !g.lo_face) ? 1 : 0;
-    const int ke = (g.nz > 1 && !g.hi_face) ? g.nz - 1 : g.nz;
-    const int kbeg = ks + blockIdx.z * CORR_KC, kend = min(kbeg + CORR_KC, ke);
-    double mv = 0.0, mp = 0.0;
-    if (i < g.nx && j < g.ny)
-    for (int k = kbeg; k < kend; ++k) {
-        const long long idx = cidx(g, i, j, k);
-        const bool interior = (i >= 1 && i <= g.nx - 2 && j >= 1 && j <= g.ny - 2 &&
-                               k >= g.k0 && k < g.k1);
-        double u, v, w;
-        if (interior) {
-            double dp_dx = (P[idx + 1] - P[idx - 1]) / cc.two_dx;
-            double dp_dy = (P[idx + g.px] - P[idx - g.px]) / cc.two_dy;
-            double dp_dz = (P[idx + g.sz] - P[idx - g.sz]) * cc.inv_2dz;
-            u = us[idx] - cc.dt_over_rho * dp_dx;
-            v = vs[idx] - cc.dt_over_rho * dp_dy;
-            w = ws[idx] - cc.dt_over_rho * dp_dz;
-            u = fmax(-100.0, fmin(100.0, u));
-            v = fmax(-100.0, fmin(100.0, v));
-            w = fmax(-100.0, fmin(100.0, w));
-            U[idx] = u;
-            V[idx] = v;
-            W[idx] = w;
-        } else {
-            u = U[idx];
-            v = V[idx];
-            w = W[idx];
-        }
-        double p = P[idx];
-        if (!isfinite(u) || !isfinite(v) || !isfinite(w) || !isfinite(p)) shbad = 1;
-        double vel = sqrt((u * u) + (v * v) + (w * w));
-        if (vel > mv) mv = vel;
-        double ap = fabs(p);
-        if (ap > mp) mp = ap;
-    }
-    mv = wave_max(mv);
-    mp = wave_max(mp);
-    if ((threadIdx.x & 63) == 0) {
-        shv[threadIdx.x >> 6] = mv;
-        shp[threadIdx.x >> 6] = mp;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = fmax(fmax(shv[0], shv[1]), fmax(shv[2], shv[3]));
-        double b = fmax(fmax(shp[0], shp[1]), fmax(shp[2], shp[3]));
-        atomicMax(&red[0], ord_enc(a));
-        atomicMax(&red[1], ord_enc(b));
-        if (shbad) atomicOr(&red[2], 1ull);
-    }
-}
-
 // Max over a full field (stats: max temperature, solver_registry.c:52-62),
 // planes [k_first, k_first + gridDim.z).
 static __global__ __launch_bounds__(256) void k_field_max(Geo g, const double* __restrict__ f,
@@ -1998,6 +1833,404 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
         for (int v = 0; v < NW; ++v) tot = fmax(tot, shs[v]);
         __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rx_finish(st, tot, it);
+    }
+}
+
+
+// ===========================================================================
+// Predictor (solver_projection.c:116-185, with compute_source_terms
+// solver_explicit_euler.c:317-333 at iter = 0 as per-row / per-column tables
+// and energy_compute_buoyancy energy_solver.c:185-196) and corrector
+// (solver_projection.c:230-250 + the boundary restore :277-278, the NaN scan
+// :281-289 and the stats of solver_registry.c:31-49), on a row-pair z-march.
+//
+// Tile = 128 (x) x 4 rows (one per wave) x kc planes, 256 threads. Each lane
+// owns an x pair and moves it with 16-B loads/stores; x neighbours come from
+// the adjacent lanes (the tile's two outer cells from one per-lane load by
+// lanes 0 and 63), z neighbours from registers (each field read once per
+// plane from HBM), y neighbours from the rows the neighbouring waves load in
+// the same step (L1/L2 hits). No LDS and no barrier: the waves of a CU run
+// independently, so memory latency hides behind the other resident waves.
+// Divisions by the constant spacings use divz (correctly rounded, bitwise
+// the reference's `/`), the reference's operation order is kept, and the
+// file is compiled with -ffp-contract=off, so u*, v*, w*, u, v, w are
+// bitwise the per-cell kernels'. Boundary cells of the tile's rows (i = 0,
+// nx - 1) are copies; the rest of the boundary shell (rows j = 0, ny - 1, the
+// z faces) is done by k_shell_copy / k_shell_stats.
+// ===========================================================================
+constexpr int PR_TY = 4;  // rows (waves) per workgroup
+
+// a / d correctly rounded, like divc, for operands that are often exactly
+// zero (derivatives of a field at rest): e = q d - a and q - e r give the
+// signed zero of a / d for a = +-0, so zeros stay on the fast path.
+__device__ __forceinline__ double divz(double a, double d, double r) {
+    const double q = a * r;
+    const double aq = fabs(q);
+    if (!(aq <= 0x1p+900 && (aq >= 0x1p-900 || aq == 0.0))) return a / d;
+    return fma(-fma(q, d, -a), r, q);
+}
+
+struct ZTile {
+    int i0, j, kb, ke, lane;
+    bool xok, in0, in1;
+    long long col;   // j * px + x offset of the pair (clamped in-row when i0 >= nx)
+    long long eoff;  // lanes 0 / 63: offset of the tile's outer x neighbour
+    bool eok;
+};
+
+__device__ __forceinline__ ZTile ztile(const SGeo& g) {
+    ZTile z;
+    const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
+    const int t = xcd_tile(blockIdx.x, nt);
+    const int tx = t % g.tiles_x;
+    const int rest = t / g.tiles_x;
+    const int ty = rest % g.tiles_y;
+    const int tz = rest / g.tiles_y;
+    z.lane = threadIdx.x & 63;
+    z.i0 = tx * 128 + 2 * z.lane;
+    z.j = ty * PR_TY + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    z.kb = g.k0 + tz * g.kc;
+    z.ke = min(z.kb + g.kc, g.k1);
+    z.xok = z.i0 < g.nx;
+    z.in0 = z.xok && z.i0 >= 1 && z.i0 <= g.nx - 2;
+    z.in1 = z.xok && z.i0 + 1 <= g.nx - 2;
+    const int ic = z.xok ? z.i0 : g.nx - 2 - ((g.nx - 2) & 1);  // even, 16-B aligned
+    z.col = (long long)z.j * g.px + ic;
+    z.eok = (z.lane == 0 && z.i0 >= 1 && z.xok) || (z.lane == 63 && z.i0 + 2 < g.nx);
+    z.eoff = (z.lane == 0) ? -1 : 2;
+    return z;
+}
+
+// x neighbours of a lane's pair: .x = left of cell i0, .y = right of i0 + 1
+__device__ __forceinline__ double2 xnbr(const ZTile& z, double2 c, double edge) {
+    const double l = __shfl_up(c.y, 1, 64);
+    const double r = __shfl_down(c.x, 1, 64);
+    return make_double2(z.lane == 0 ? edge : l, z.lane == 63 ? edge : r);
+}
+
+struct PredCoef2 {
+    double two_dx, two_dy, inv_2dz;  // first derivatives
+    double dx_sq, dy_sq, inv_dz2;    // second derivatives
+    double r_two_dx, r_two_dy, r_dx_sq, r_dy_sq;  // RN(1 / divisor) for divz
+    double dt, nu;
+    double beta, T_ref, g0, g1, g2;
+};
+
+// solver_projection.c:121-182 for one cell: c = centre (u, v, w), f = the
+// field the output belongs to (0, 1, 2) with its 6 neighbours
+__device__ __forceinline__ double pred_cell(const PredCoef2& pc, double u, double v, double w,
+                                            double fc, double xm, double xp, double ym,
+                                            double yp, double zm, double zp, double src) {
+    const double d_dx = divz(xp - xm, pc.two_dx, pc.r_two_dx);
+    const double d_dy = divz(yp - ym, pc.two_dy, pc.r_two_dy);
+    const double d_dz = (zp - zm) * pc.inv_2dz;
+    const double conv = u * d_dx + v * d_dy + w * d_dz;
+    const double d2x = divz(xp - 2.0 * fc + xm, pc.dx_sq, pc.r_dx_sq);
+    const double d2y = divz(yp - 2.0 * fc + ym, pc.dy_sq, pc.r_dy_sq);
+    const double d2z = (zp - 2.0 * fc + zm) * pc.inv_dz2;
+    const double visc = pc.nu * (d2x + d2y + d2z);
+    const double a = fc + pc.dt * (-conv + visc + src);
+    return fmax(-100.0, fmin(100.0, a));
+}
+
+// The loads of plane k + 1 (the z+ centre row, the two y rows, the x-edge
+// cells, T) are issued while plane k is computed: two register slots
+// alternate over an unrolled pair of planes, so a slot is first read one
+// step after its loads were issued.
+struct PredBundle {
+    double2 pp[3], ym[3], yp[3], tc;
+    double e[3];
+};
+
+// PF: 0 = each plane's loads issued in its own step, 1 = one plane ahead in
+// two alternating register slots (more VGPRs, two waves per SIMD).
+template <int PF>
+constexpr int pred_min_waves() { return PF ? 2 : 4; }
+
+template <bool BUOY, int PF>
+static __global__ __launch_bounds__(64 * PR_TY, pred_min_waves<PF>()) void k_pred2(
+    SGeo g, PredCoef2 pc, const double* __restrict__ U, const double* __restrict__ V,
+    const double* __restrict__ W, const double* __restrict__ T,
+    const double* __restrict__ src_u_row, const double* __restrict__ src_v_col,
+    double* __restrict__ us, double* __restrict__ vs, double* __restrict__ ws) {
+    const ZTile z = ztile(g);
+    if (z.j < 1 || z.j > g.ny - 2) return;  // boundary rows: k_shell_copy
+    const double su = src_u_row[z.j];
+    const double sv0 = z.xok ? src_v_col[z.i0] : 0.0;
+    const double sv1 = z.in1 ? src_v_col[z.i0 + 1] : 0.0;
+    const double* F[3] = {U, V, W};
+    double* O[3] = {us, vs, ws};
+    const long long idx0 = (long long)z.kb * g.ps + z.col;
+    auto issue = [&](PredBundle& b, long long idx) __attribute__((always_inline)) {
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            b.pp[f] = ld2(F[f], idx + g.sz);
+            b.ym[f] = ld2(F[f], idx - g.px);
+            b.yp[f] = ld2(F[f], idx + g.px);
+            b.e[f] = z.eok ? F[f][idx + z.eoff] : 0.0;
+        }
+        b.tc = BUOY ? ld2(T, idx) : make_double2(0.0, 0.0);
+    };
+    double2 pm[3], pc3[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        pm[f] = ld2(F[f], idx0 - g.sz);
+        pc3[f] = ld2(F[f], idx0);
+    }
+    // plane k from bundle b; the loads of plane k + 1 go to nb first
+    auto step = [&](const PredBundle& b0, PredBundle& nb, int k) __attribute__((always_inline)) {
+        const long long idx = idx0 + (long long)(k - z.kb) * g.ps;
+        PredBundle cur;
+        if (PF) {
+            if (k + 1 < z.ke) issue(nb, idx + g.ps);
+        } else {
+            issue(cur, idx);
+        }
+        const PredBundle& b = PF ? b0 : cur;
+        const double u0 = pc3[0].x, u1 = pc3[0].y;
+        const double v0 = pc3[1].x, v1 = pc3[1].y;
+        const double w0 = pc3[2].x, w1 = pc3[2].y;
+        // sources: compute_source_terms + energy_compute_buoyancy
+        // (solver_explicit_euler.c:317-333, energy_solver.c:185-196)
+        double s0[3] = {su, sv0, 0.0}, s1[3] = {su, sv1, 0.0};
+        if (BUOY) {
+            const double dT0 = b.tc.x - pc.T_ref, dT1 = b.tc.y - pc.T_ref;
+            s0[0] += -pc.beta * dT0 * pc.g0;
+            s0[1] += -pc.beta * dT0 * pc.g1;
+            s0[2] += -pc.beta * dT0 * pc.g2;
+            s1[0] += -pc.beta * dT1 * pc.g0;
+            s1[1] += -pc.beta * dT1 * pc.g1;
+            s1[2] += -pc.beta * dT1 * pc.g2;
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const double2 lr = xnbr(z, pc3[f], b.e[f]);
+            double2 o = pc3[f];  // boundary cells: u* = u
+            const double r0 = pred_cell(pc, u0, v0, w0, pc3[f].x, lr.x, pc3[f].y, b.ym[f].x,
+                                        b.yp[f].x, pm[f].x, b.pp[f].x, s0[f]);
+            const double r1 = pred_cell(pc, u1, v1, w1, pc3[f].y, pc3[f].x, lr.y, b.ym[f].y,
+                                        b.yp[f].y, pm[f].y, b.pp[f].y, s1[f]);
+            if (z.in0) o.x = r0;
+            if (z.in1) o.y = r1;
+            if (z.xok) st2(O[f], idx, o);
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            pm[f] = pc3[f];
+            pc3[f] = b.pp[f];
+        }
+    };
+    PredBundle A, B;
+    if constexpr (PF != 0) {
+        issue(A, idx0);
+        int k = z.kb;
+        for (; k + 1 < z.ke; k += 2) {
+            step(A, B, k);
+            step(B, A, k + 1);
+        }
+        if (k < z.ke) step(A, B, k);
+    } else {
+        for (int k = z.kb; k < z.ke; ++k) step(A, B, k);
+    }
+}
+
+// Boundary shell of the predictor: u* = u on every cell the z-march does not
+// write (rows j = 0, ny - 1 of every plane, the x edges, the z faces).
+static __global__ __launch_bounds__(256) void k_shell_copy(Geo g, const double* __restrict__ U,
+                                                           const double* __restrict__ V,
+                                                           const double* __restrict__ W,
+                                                           double* __restrict__ us,
+                                                           double* __restrict__ vs,
+                                                           double* __restrict__ ws) {
+    const long long total = shell_total(g);
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        int i, j, k;
+        bool zlo, zhi;
+        shell_cell(g, e, i, j, k, zlo, zhi);
+        const long long d = cidx(g, i, j, k);
+        us[d] = U[d];
+        vs[d] = V[d];
+        ws[d] = W[d];
+    }
+}
+
+// Corrector (solver_projection.c:230-250) on the interior rows and planes +
+// NaN/Inf scan and max |u|, max |p| of those cells; boundary cells of the
+// tile's rows keep u (== u*) and join the scan. The rest of the shell is
+// scanned by k_shell_stats. red[0] = max |u| (encoded), [1] = max |p|,
+// [2] = non-finite flag.
+struct CorrCoef2 {
+    double two_dx, two_dy, inv_2dz;
+    double r_two_dx, r_two_dy;
+    double dt_over_rho;
+};
+
+__device__ __forceinline__ void corr_reduce(double mv, double mp, bool bad,
+                                            unsigned long long* red) {
+    __shared__ double shv[PR_TY], shp[PR_TY];
+    __shared__ int shbad;
+    if (threadIdx.x == 0) shbad = 0;
+    __syncthreads();
+    mv = wave_max(mv);
+    mp = wave_max(mp);
+    if (bad) shbad = 1;
+    if ((threadIdx.x & 63) == 0) {
+        shv[threadIdx.x >> 6] = mv;
+        shp[threadIdx.x >> 6] = mp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = shv[0], b = shp[0];
+        for (int q = 1; q < PR_TY; ++q) {
+            a = fmax(a, shv[q]);
+            b = fmax(b, shp[q]);
+        }
+        atomicMax(&red[0], ord_enc(a));
+        atomicMax(&red[1], ord_enc(b));
+        if (shbad) atomicOr(&red[2], 1ull);
+    }
+}
+
+__device__ __forceinline__ void cell_stats(double u, double v, double w, double p, double& mv,
+                                           double& mp, bool& bad) {
+    if (!isfinite(u) || !isfinite(v) || !isfinite(w) || !isfinite(p)) bad = true;
+    const double vel = sqrt((u * u) + (v * v) + (w * w));  // solver_registry.c:31-49
+    if (vel > mv) mv = vel;
+    const double ap = fabs(p);
+    if (ap > mp) mp = ap;
+}
+
+struct CorrBundle {
+    double2 pp, ym, yp, a, b, c;
+    double e;
+};
+
+// PF as in k_pred2: 1 = the loads of plane k + 1 are issued during plane k
+template <int PF>
+static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
+    SGeo g, CorrCoef2 cc, const double* __restrict__ us, const double* __restrict__ vs,
+    const double* __restrict__ ws, const double* __restrict__ P, double* __restrict__ U,
+    double* __restrict__ V, double* __restrict__ W, unsigned long long* red) {
+    const ZTile z = ztile(g);
+    double mv = 0.0, mp = 0.0;
+    bool bad = false;
+    if (z.j >= 1 && z.j <= g.ny - 2) {  // wave-uniform
+        const long long idx0 = (long long)z.kb * g.ps + z.col;
+        double2 pm = ld2(P, idx0 - g.sz), pc = ld2(P, idx0);
+        auto issue = [&](CorrBundle& q, long long idx) __attribute__((always_inline)) {
+            q.pp = ld2(P, idx + g.sz);
+            q.ym = ld2(P, idx - g.px);
+            q.yp = ld2(P, idx + g.px);
+            q.e = z.eok ? P[idx + z.eoff] : 0.0;
+            q.a = ld2(us, idx);
+            q.b = ld2(vs, idx);
+            q.c = ld2(ws, idx);
+        };
+        auto step = [&](const CorrBundle& q0, CorrBundle& nq, int k) __attribute__((always_inline)) {
+            const long long idx = idx0 + (long long)(k - z.kb) * g.ps;
+            CorrBundle cur;
+            if (PF) {
+                if (k + 1 < z.ke) issue(nq, idx + g.ps);
+            } else {
+                issue(cur, idx);
+            }
+            const CorrBundle& q = PF ? q0 : cur;
+            const double2 lr = xnbr(z, pc, q.e);
+            const double left = lr.x, right = lr.y;
+            double2 nu = q.a, nv = q.b, nw = q.c;  // boundary cells: u = u* (== u)
+            {
+                const double dp_dx = divz(pc.y - left, cc.two_dx, cc.r_two_dx);
+                const double dp_dy = divz(q.yp.x - q.ym.x, cc.two_dy, cc.r_two_dy);
+                const double dp_dz = (q.pp.x - pm.x) * cc.inv_2dz;
+                const double x0 = fmax(-100.0, fmin(100.0, q.a.x - cc.dt_over_rho * dp_dx));
+                const double y0 = fmax(-100.0, fmin(100.0, q.b.x - cc.dt_over_rho * dp_dy));
+                const double w0 = fmax(-100.0, fmin(100.0, q.c.x - cc.dt_over_rho * dp_dz));
+                if (z.in0) {
+                    nu.x = x0;
+                    nv.x = y0;
+                    nw.x = w0;
+                }
+            }
+            {
+                const double dp_dx = divz(right - pc.x, cc.two_dx, cc.r_two_dx);
+                const double dp_dy = divz(q.yp.y - q.ym.y, cc.two_dy, cc.r_two_dy);
+                const double dp_dz = (q.pp.y - pm.y) * cc.inv_2dz;
+                const double x1 = fmax(-100.0, fmin(100.0, q.a.y - cc.dt_over_rho * dp_dx));
+                const double y1 = fmax(-100.0, fmin(100.0, q.b.y - cc.dt_over_rho * dp_dy));
+                const double w1 = fmax(-100.0, fmin(100.0, q.c.y - cc.dt_over_rho * dp_dz));
+                if (z.in1) {
+                    nu.y = x1;
+                    nv.y = y1;
+                    nw.y = w1;
+                }
+            }
+            if (z.xok) {
+                st2(U, idx, nu);
+                st2(V, idx, nv);
+                st2(W, idx, nw);
+                cell_stats(nu.x, nv.x, nw.x, pc.x, mv, mp, bad);
+                if (z.i0 + 1 < g.nx) cell_stats(nu.y, nv.y, nw.y, pc.y, mv, mp, bad);
+            }
+            pm = pc;
+            pc = q.pp;
+        };
+        CorrBundle A, B;
+        if constexpr (PF != 0) {
+            issue(A, idx0);
+            int k = z.kb;
+            for (; k + 1 < z.ke; k += 2) {
+                step(A, B, k);
+                step(B, A, k + 1);
+            }
+            if (k < z.ke) step(A, B, k);
+        } else {
+            for (int k = z.kb; k < z.ke; ++k) step(A, B, k);
+        }
+    }
+    corr_reduce(mv, mp, bad, red);
+}
+
+// Stats over the boundary shell cells the corrector's z-march does not visit
+// (rows j = 0, ny - 1 of the owned planes, the global z faces): u, v, w are
+// the caller's boundary values there. Planes [ks, ke) as in the corrector.
+static __global__ __launch_bounds__(256) void k_shell_stats(Geo g, const double* __restrict__ U,
+                                                            const double* __restrict__ V,
+                                                            const double* __restrict__ W,
+                                                            const double* __restrict__ P,
+                                                            unsigned long long* red) {
+    __shared__ double shv[4], shp[4];
+    __shared__ int shbad;
+    if (threadIdx.x == 0) shbad = 0;
+    __syncthreads();
+    const int ks = (g.nz > 1 && !g.lo_face) ? 1 : 0;
+    const int ke = (g.nz > 1 && !g.hi_face) ? g.nz - 1 : g.nz;
+    const long long total = shell_total(g);
+    double mv = 0.0, mp = 0.0;
+    bool bad = false;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        int i, j, k;
+        bool zlo, zhi;
+        shell_cell(g, e, i, j, k, zlo, zhi);
+        // the z-march covers i = 0 / nx - 1 of its rows on interior planes
+        const bool marched = (j >= 1 && j <= g.ny - 2 && k >= g.k0 && k < g.k1);
+        if (k < ks || k >= ke || marched) continue;
+        const long long d = cidx(g, i, j, k);
+        cell_stats(U[d], V[d], W[d], P[d], mv, mp, bad);
+    }
+    mv = wave_max(mv);
+    mp = wave_max(mp);
+    if (bad) shbad = 1;
+    if ((threadIdx.x & 63) == 0) {
+        shv[threadIdx.x >> 6] = mv;
+        shp[threadIdx.x >> 6] = mp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicMax(&red[0], ord_enc(fmax(fmax(shv[0], shv[1]), fmax(shv[2], shv[3]))));
+        atomicMax(&red[1], ord_enc(fmax(fmax(shp[0], shp[1]), fmax(shp[2], shp[3]))));
+        if (shbad) atomicOr(&red[2], 1ull);
     }
 }
 

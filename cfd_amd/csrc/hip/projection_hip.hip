@@ -702,6 +702,17 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         rg.tiles_z = (nint_k + rg.kc - 1) / rg.kc;
         n_partials = std::max(n_partials, rg.tiles_x * rg.tiles_y * rg.tiles_z);
     }
+    {   // predictor / corrector: 128 x PR_TY x kc tiles, >= ~8 workgroups per CU
+        SGeo& pg = c->pgeo;
+        pg = sg;
+        pg.kmode = 0;
+        pg.tiles_x = (int)((nx + 127) / 128);
+        pg.tiles_y = (int)((ny + PR_TY - 1) / PR_TY);
+        const long long xy = (long long)pg.tiles_x * pg.tiles_y;
+        const long long zt = std::max(1LL, (8LL * c->grid_cap / 8 + xy - 1) / xy);
+        pg.kc = (int)std::max<long long>(1, (nint_k + zt - 1) / zt);
+        pg.tiles_z = (nint_k + pg.kc - 1) / pg.kc;
+    }
     c->split_b = (c->nranks > 1 && nint_k >= 3) ? 1 : 0;
     if (c->split_b) {
         // sweep B on slabs: the two edge planes (what the neighbours need)
@@ -1125,13 +1136,17 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     HIP_TRY(hipMemcpyAsync(c->src_v_col, c->h_src_v.data(), nx * sizeof(double),
                            hipMemcpyHostToDevice, c->stream));
 
-    PredCoef pc;
+    PredCoef2 pc;
     pc.two_dx = 2.0 * dx;
     pc.two_dy = 2.0 * dy;
     pc.inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * dz) : 0.0;
     pc.dx_sq = dx * dx;
     pc.dy_sq = dy * dy;
     pc.inv_dz2 = (nz > 1 && g->dz) ? 1.0 / (dz * dz) : 0.0;
+    pc.r_two_dx = 1.0 / pc.two_dx;
+    pc.r_two_dy = 1.0 / pc.two_dy;
+    pc.r_dx_sq = 1.0 / pc.dx_sq;
+    pc.r_dy_sq = 1.0 / pc.dy_sq;
     pc.dt = dt;
     pc.nu = prm->mu;
     pc.beta = prm->beta;
@@ -1139,18 +1154,24 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     pc.g0 = prm->gravity[0];
     pc.g1 = prm->gravity[1];
     pc.g2 = prm->gravity[2];
-    const dim3 cg = cell_grid(c);
+    const unsigned npg = (unsigned)(c->pgeo.tiles_x * c->pgeo.tiles_y * c->pgeo.tiles_z);
     // slabs: the neighbours' planes of everything the stencils read
     ST_TRY(halo(c, {c->u, c->v, c->w, c->p}));
     if (buoy || energy) ST_TRY(halo(c, {c->T}));
     timed(c, HIP_KT_PREDICTOR, [&] {
+        // PF = 0: one plane's loads per step (the plane-ahead schedule
+        // measured slower, profiles/r02_step_kernels.jsonl)
         if (buoy)
-            hipExtLaunchKernelGGL(k_predictor<true>, cg, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, pc, c->u,
-                               c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
+            hipExtLaunchKernelGGL((k_pred2<true, 0>), dim3(npg), dim3(64 * PR_TY), 0, c->stream,
+                                  c->ta, c->tb, 0, c->pgeo, pc, c->u, c->v, c->w, c->T,
+                                  c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
         else
-            hipExtLaunchKernelGGL(k_predictor<false>, cg, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, pc, c->u,
-                               c->v, c->w, c->T, c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
+            hipExtLaunchKernelGGL((k_pred2<false, 0>), dim3(npg), dim3(64 * PR_TY), 0, c->stream,
+                                  c->ta, c->tb, 0, c->pgeo, pc, c->u, c->v, c->w, c->T,
+                                  c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
     });
+    hipExtLaunchKernelGGL(k_shell_copy, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
+                          c->tb, 0, c->geo, c->u, c->v, c->w, c->us, c->vs, c->ws);
     HIP_TRY(hipGetLastError());
     ST_TRY(halo(c, {c->ws}));  // d(w*)/dz of the divergence
 
@@ -1193,19 +1214,21 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
         return ps;
     }
 
-    CorrCoef cc;
+    CorrCoef2 cc;
     cc.two_dx = 2.0 * dx;
     cc.two_dy = 2.0 * dy;
     cc.inv_2dz = pc.inv_2dz;
+    cc.r_two_dx = pc.r_two_dx;
+    cc.r_two_dy = pc.r_two_dy;
     cc.dt_over_rho = dt / rho;
     hipExtLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->red);
     timed(c, HIP_KT_CORRECTOR, [&] {
-        const int ks = (c->nz > 1 && !c->geo.lo_face) ? 1 : 0;
-        const int ke = (c->nz > 1 && !c->geo.hi_face) ? (int)c->nz - 1 : (int)c->nz;
-        const dim3 cgz(cg.x, cg.y, (unsigned)((ke - ks + CORR_KC - 1) / CORR_KC));
-        hipExtLaunchKernelGGL(k_corrector, cgz, dim3(256), 0, c->stream, c->ta, c->tb, 0, c->geo, cc, c->us, c->vs,
-                           c->ws, c->pn, c->u, c->v, c->w, c->red);
+        hipExtLaunchKernelGGL((k_corr2<0>), dim3(npg), dim3(64 * PR_TY), 0, c->stream, c->ta,
+                              c->tb, 0, c->pgeo, cc, c->us, c->vs, c->ws, c->pn, c->u, c->v, c->w,
+                              c->red);
     });
+    hipExtLaunchKernelGGL(k_shell_stats, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
+                          c->tb, 0, c->geo, c->u, c->v, c->w, c->pn, c->red);
     std::swap(c->p, c->pn);  // memcpy(field->p, p_new) (solver_projection.c:253)
     if (energy) ST_TRY(ctx_energy_step(c, g, prm, true));  // solver_projection.c:255-274
     ctx_queue_max_T(c);
