@@ -191,6 +191,11 @@ NS_SOLVER_BACKEND_SCALAR = 0  # ns_solver_backend_t (navier_stokes_solver.h:172-
 NS_SOLVER_BACKEND_SIMD = 1
 NS_SOLVER_BACKEND_OMP = 2
 NS_SOLVER_BACKEND_CUDA = 3
+# hip_poisson_bc_t (include/cfd_hip/projection_hip.h)
+HIP_POISSON_BC_NEUMANN = 0
+HIP_POISSON_BC_NONE = 1
+HIP_POISSON_BC_FIXED = 2
+
 POISSON_BACKEND_AUTO = 0
 POISSON_BACKEND_SCALAR = 1
 POISSON_BACKEND_OMP = 2

@@ -181,6 +181,9 @@ def _bind_hip(lib) -> None:
          C.c_double, C.c_int)
     _sig(lib, "hip_proj_poisson_solve", C.c_int, V, C.c_int, A.c_double_p, A.c_double_p,
          C.c_double, C.c_double, C.c_double, P(A.PoissonParams), P(A.PoissonStats))
+    _sig(lib, "hip_proj_poisson_solve_ex", C.c_int, V, C.c_int, A.c_double_p, A.c_double_p,
+         C.c_double, C.c_double, C.c_double, P(A.PoissonParams), P(A.PoissonStats), C.c_int,
+         A.c_double_p)
     _sig(lib, "hip_proj_slab_layout", C.c_int, C.c_size_t, C.c_int, C.c_int, P(C.c_size_t),
          P(C.c_size_t))
     _sig(lib, "hip_proj_comm_unique_id", C.c_int, C.c_char_p)

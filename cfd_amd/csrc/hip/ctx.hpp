@@ -87,6 +87,12 @@ struct hip_proj_ctx {
     // them; the CG needs zero wall cells in r and the p ring (lagged-BC
     // semantics), so the next CG solve clears them first.
     int cg_scratch_dirty = 0;
+    // boundary handling of the pressure solve in progress (hip_poisson_bc_t):
+    // NEUMANN = the reference's default apply_bc; NONE = boundary cells of x
+    // never written (the caller's apply_bc runs on the host); FIXED = after
+    // every relaxation iteration the shell is copied from bcfix
+    int poisson_bc = 0;
+    double* bcfix = nullptr;
     double* Tn = nullptr;  // energy equation output (swapped with T)
     double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated
     double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3

@@ -139,8 +139,10 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         c->cg_scratch_dirty = 0;
     }
     ST_TRY(halo(c, {x}));
-    // poisson_solver_apply_bc(x) at solve start (linear_solver_cg.c:320)
-    launch_bc(c, x, 0, dv);
+    // poisson_solver_apply_bc(x) at solve start (linear_solver_cg.c:320); a
+    // caller override runs on the host around the device solve instead
+    const bool neumann = (c->poisson_bc == HIP_POISSON_BC_NEUMANN);
+    if (neumann) launch_bc(c, x, 0, dv);
     timed(c, HIP_KT_CG_SETUP, [&] {
         const double* rhs_in = (src == RHS_FROM_VELOCITY) ? nullptr : c->rhs;
         if (src == RHS_FROM_VELOCITY) {
@@ -253,7 +255,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     }
     const bool stagnated = (s.status == ST_STAGNATED);
     // final poisson_solver_apply_bc (cg.c:447); the breakdown exit skips it.
-    if (final_bc && !stagnated && !(s.iterations == 0 && s.status == ST_CONVERGED))
+    if (final_bc && neumann && !stagnated && !(s.iterations == 0 && s.status == ST_CONVERGED))
         launch_bc(c, x, 0, dv);
     ST_TRY(halo(c, {x}));
     c->pstats.status = (poisson_solver_status_t)s.status;
@@ -375,8 +377,13 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             ST_TRY(finish(it));
         }
         ST_TRY(halo(c, {xo}));
+        // the iteration's apply_bc: Neumann (linear_solver_redblack.c:139,
+        // linear_solver_jacobi.c:118), or the caller's fixed boundary values,
+        // or x's own boundary kept
+        const double* shell_src = (c->poisson_bc == HIP_POISSON_BC_FIXED) ? c->bcfix : xi;
+        const int shell_mode = (c->poisson_bc == HIP_POISSON_BC_NEUMANN) ? 1 : 0;
         hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
-                              c->tb, 0, c->geo, c->rxst, nullptr, xo, 1);
+                              c->tb, 0, c->geo, c->rxst, shell_src, xo, shell_mode);
         return CFD_SUCCESS;
     };
     // iterations 0..max_iter: sweep it also yields the residual after it - 1
@@ -432,7 +439,8 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
     rc.omega = (omega_in <= 0.0) ? optimal_omega(c->nx, c->ny, c->nzg, dx, dy, dz) : omega_in;
     rc.rdx2 = 1.0 / rc.dx2;
     rc.rdy2 = 1.0 / rc.dy2;
-    if ((c->sweep_ty == 16 || c->sweep_ty == 8) && max_iter > 0 && c->cfg.relax_two_pass != 1)
+    if ((c->sweep_ty == 16 || c->sweep_ty == 8) && max_iter > 0 &&
+        (c->cfg.relax_two_pass != 1 || c->poisson_bc != HIP_POISSON_BC_NEUMANN))
         return relax_solve_fused(c, method, rc, rel_tol, abs_tol, max_iter, check_interval);
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
     const DirVals dv{};
@@ -1329,8 +1337,46 @@ cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* c, int method, double* x, co
                                     double dx, double dy, double dz,
                                     const poisson_solver_params_t* params,
                                     poisson_solver_stats_t* stats) {
+    return hip_proj_poisson_solve_ex(c, method, x, rhs, dx, dy, dz, params, stats,
+                                     HIP_POISSON_BC_NEUMANN, nullptr);
+}
+
+static cfd_status_t poisson_solve_impl(hip_proj_ctx_t* c, int method, double* x,
+                                       const double* rhs, double dx, double dy, double dz,
+                                       const poisson_solver_params_t* params,
+                                       poisson_solver_stats_t* stats);
+
+cfd_status_t hip_proj_poisson_solve_ex(hip_proj_ctx_t* c, int method, double* x,
+                                       const double* rhs, double dx, double dy, double dz,
+                                       const poisson_solver_params_t* params,
+                                       poisson_solver_stats_t* stats, int bc_mode,
+                                       const double* bc_values) {
     if (!c || !x || !rhs) return CFD_ERROR_INVALID;
+    if (bc_mode != HIP_POISSON_BC_NEUMANN && bc_mode != HIP_POISSON_BC_NONE &&
+        bc_mode != HIP_POISSON_BC_FIXED)
+        return CFD_ERROR_INVALID;
+    if (bc_mode == HIP_POISSON_BC_FIXED && !bc_values) return CFD_ERROR_INVALID;
+    if (bc_mode != HIP_POISSON_BC_NEUMANN && dist(c)) {
+        set_err(CFD_ERROR_UNSUPPORTED, "hip_proj_poisson_solve_ex: caller BCs on Z-slabs");
+        return CFD_ERROR_UNSUPPORTED;
+    }
     HIP_TRY(hipSetDevice(c->device));
+    if (bc_mode == HIP_POISSON_BC_FIXED) {
+        if (!c->bcfix) ST_TRY(dalloc(c, &c->bcfix, field_elems(c)));
+        HIP_TRY(hipMemcpy2DAsync(c->bcfix, c->px * sizeof(double), bc_values,
+                                 c->nx * sizeof(double), c->nx * sizeof(double), c->ny * c->nz,
+                                 hipMemcpyHostToDevice, c->stream));
+    }
+    c->poisson_bc = bc_mode;
+    const cfd_status_t s = poisson_solve_impl(c, method, x, rhs, dx, dy, dz, params, stats);
+    c->poisson_bc = HIP_POISSON_BC_NEUMANN;
+    return s;
+}
+
+static cfd_status_t poisson_solve_impl(hip_proj_ctx_t* c, int method, double* x,
+                                       const double* rhs, double dx, double dy, double dz,
+                                       const poisson_solver_params_t* params,
+                                       poisson_solver_stats_t* stats) {
     double rel = 1e-6, abs_tol = 1e-10, omega = 0.0;
     int maxit = (method == HIP_POISSON_JACOBI) ? 2000 : 5000, ci = 1;
     if (params) {

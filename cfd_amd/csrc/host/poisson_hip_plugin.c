@@ -9,6 +9,18 @@
  * semantics: solve uploads x and rhs, runs the whole iteration in HBM, and
  * downloads x; iterate and apply_bc stay NULL.
  *
+ * A caller may override solver->apply_bc (test_poisson_3d.c:274); the
+ * reference's CUDA backends ignore it, these honour it:
+ *  - CG applies the BC only at solve start and end (linear_solver_cg.c:320,
+ *    447), so the override runs on the host around the device solve, which
+ *    then never writes boundary cells (HIP_POISSON_BC_NONE): any override;
+ *  - RB-SOR / Jacobi apply it after every iteration. An override that
+ *    leaves the interior alone and writes x-independent boundary values
+ *    (Dirichlet; "keep the caller's boundary"; any mix per cell) is found by
+ *    calling it on two different probe arrays (probe_bc); the boundary it
+ *    leaves is then imposed on the device after every iteration
+ *    (HIP_POISSON_BC_FIXED). Other overrides are CFD_ERROR_UNSUPPORTED.
+ *
  * Numerics follow the CPU reference the HIP kernels are pinned to (lagged-BC CG,
  * linear_solver_cg.c:290-461; RB-SOR with the odd colour first and the L-inf
  * check, linear_solver_redblack.c:80-147 + linear_solver.c:397-485; Jacobi,
@@ -19,6 +31,7 @@
 #include "cfd_hip/projection_hip.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 extern void cfd_set_error(cfd_status_t status, const char* message) __attribute__((weak));
 
@@ -63,15 +76,95 @@ static void phip_destroy(poisson_solver_t* solver) {
     solver->context = NULL;
 }
 
+static int interior_cell(const poisson_solver_t* s, size_t e) {
+    const size_t nx = s->nx, ny = s->ny, nz = s->nz < 1 ? 1 : s->nz;
+    const size_t i = e % nx, j = (e / nx) % ny, k = e / (nx * ny);
+    const int kin = (nz > 1) ? (k >= 1 && k <= nz - 2) : 1;
+    return i >= 1 && i <= nx - 2 && j >= 1 && j <= ny - 2 && kin;
+}
+
+/* The boundary an apply_bc override leaves after every relaxation iteration,
+ * found by running it on two unrelated probe arrays. It must leave interior
+ * cells alone; each boundary cell is either written with the same value in
+ * both probes (that value is kept) or left untouched in both (the cell then
+ * keeps keep[e]: x's own value for RB-SOR, whose sweeps never write boundary
+ * cells, or x_temp's for Jacobi, whose memcpy(x, x_temp) brings it in,
+ * linear_solver_jacobi.c:118). Returns the full-size array of boundary values
+ * (interior entries unused), or NULL for an override outside this class. */
+static double probe_a(size_t e) { return 0.5 + (double)(e % 97) * 0.015625; }
+static double probe_b(size_t e) { return -3.0 - (double)(e % 89) * 0.0078125; }
+
+static double* probe_bc(poisson_solver_t* s, const double* keep) {
+    const size_t n = s->nx * s->ny * (s->nz < 1 ? 1 : s->nz);
+    double* a = (double*)malloc(n * sizeof(double));
+    double* b = (double*)malloc(n * sizeof(double));
+    if (!a || !b) {
+        free(a);
+        free(b);
+        return NULL;
+    }
+    for (size_t e = 0; e < n; e++) {
+        a[e] = probe_a(e);
+        b[e] = probe_b(e);
+    }
+    s->apply_bc(s, a);
+    s->apply_bc(s, b);
+    int ok = 1;
+    for (size_t e = 0; e < n && ok; e++) {
+        const int untouched = a[e] == probe_a(e) && b[e] == probe_b(e);
+        if (interior_cell(s, e)) ok = untouched;
+        else if (untouched) a[e] = keep[e];
+        else ok = memcmp(&a[e], &b[e], sizeof(double)) == 0;
+    }
+    free(b);
+    if (!ok) {
+        free(a);
+        return NULL;
+    }
+    return a;
+}
+
 static cfd_status_t phip_solve(poisson_solver_t* solver, double* x, double* x_temp,
                                const double* rhs, poisson_solver_stats_t* stats) {
-    (void)x_temp; /* every working vector lives in HBM */
+    /* every working vector lives in HBM; x_temp only supplies the boundary
+     * a Jacobi apply_bc override leaves untouched */
     if (!solver || !x || !rhs) return CFD_ERROR_INVALID;
     poisson_hip_ctx* pc = (poisson_hip_ctx*)solver->context;
     if (!pc || !pc->ctx) return CFD_ERROR_INVALID;
     double dz = (solver->nz > 1) ? solver->dz : 0.0;
-    return hip_proj_poisson_solve(pc->ctx, pc->method, x, rhs, solver->dx, solver->dy, dz,
-                                  &solver->params, stats);
+    if (pc->method == HIP_POISSON_JACOBI && !x_temp) {
+        perr(CFD_ERROR_INVALID, "Jacobi requires a temp buffer"); /* linear_solver_jacobi.c:83-85 */
+        return CFD_ERROR_INVALID;
+    }
+    if (!solver->apply_bc)
+        return hip_proj_poisson_solve(pc->ctx, pc->method, x, rhs, solver->dx, solver->dy, dz,
+                                      &solver->params, stats);
+    if (pc->method == HIP_POISSON_CG) {
+        poisson_solver_stats_t st;
+        memset(&st, 0, sizeof(st));
+        solver->apply_bc(solver, x); /* linear_solver_cg.c:320 */
+        cfd_status_t r = hip_proj_poisson_solve_ex(pc->ctx, pc->method, x, rhs, solver->dx,
+                                                   solver->dy, dz, &solver->params, &st,
+                                                   HIP_POISSON_BC_NONE, NULL);
+        /* :447, skipped by the breakdown exits and the converged-at-start return */
+        const int early = st.status == POISSON_STAGNATED ||
+                          (st.iterations == 0 && st.status == POISSON_CONVERGED);
+        if ((r == CFD_SUCCESS || r == CFD_ERROR_MAX_ITER) && !early) solver->apply_bc(solver, x);
+        if (stats) *stats = st;
+        return r;
+    }
+    double* vals = probe_bc(solver, pc->method == HIP_POISSON_JACOBI ? x_temp : x);
+    if (!vals) {
+        perr(CFD_ERROR_UNSUPPORTED,
+             "GPU Poisson: a relaxation apply_bc override must leave the interior alone and, "
+             "per boundary cell, keep it or write an x-independent value; use CG otherwise");
+        return CFD_ERROR_UNSUPPORTED;
+    }
+    cfd_status_t r = hip_proj_poisson_solve_ex(pc->ctx, pc->method, x, rhs, solver->dx,
+                                               solver->dy, dz, &solver->params, stats,
+                                               HIP_POISSON_BC_FIXED, vals);
+    free(vals);
+    return r;
 }
 
 static poisson_solver_t* make(const char* name, const char* desc,

@@ -237,6 +237,31 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* ctx, int meth
                                                    const poisson_solver_params_t* params,
                                                    poisson_solver_stats_t* stats);
 
+/* Boundary handling of hip_proj_poisson_solve_ex. The reference solvers call
+ * poisson_solver_apply_bc (linear_solver.c:348-392): the caller's
+ * solver->apply_bc when set (test_poisson_3d.c:274), else Neumann.
+ *   NEUMANN  the default apply_bc, on the device (what hip_proj_poisson_solve does);
+ *   NONE     boundary cells of x are never written on the device: CG only
+ *            reads them (linear_solver_cg.c applies the BC at :320 and :447,
+ *            which the caller then runs on the host around the solve), and
+ *            relaxation iterations keep x's own boundary;
+ *   FIXED    after every relaxation iteration (linear_solver_redblack.c:139,
+ *            linear_solver_jacobi.c:118) the boundary shell of x is set from
+ *            bc_values (nx*ny*nz host doubles, only the shell read): an
+ *            apply_bc that writes x-independent values, e.g. Dirichlet. */
+typedef enum {
+    HIP_POISSON_BC_NEUMANN = 0,
+    HIP_POISSON_BC_NONE = 1,
+    HIP_POISSON_BC_FIXED = 2
+} hip_poisson_bc_t;
+
+CFD_HIP_EXPORT cfd_status_t hip_proj_poisson_solve_ex(hip_proj_ctx_t* ctx, int method, double* x,
+                                                      const double* rhs, double dx, double dy,
+                                                      double dz,
+                                                      const poisson_solver_params_t* params,
+                                                      poisson_solver_stats_t* stats, int bc_mode,
+                                                      const double* bc_values);
+
 /* ---- Z-slab multi-GPU ------------------------------------------------------
  * The reference runs one device per simulation (solver_projection_gpu.cu has
  * no decomposition). Here the nz-2 interior planes of the

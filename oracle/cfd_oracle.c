@@ -30,6 +30,7 @@
 static int g_threads = 1;
 static int g_poisson_cap = 0; /* >0: timing-only sample, CG capped and accepted */
 static int g_have_pparams = 0;
+static int g_gpu_rhs = 0;     /* 1: rhs = div / dt, the reference GPU's (solver_projection_gpu.cu:706-707) */
 static poisson_solver_params_t g_pparams;
 static double g_phase_ms[4];
 
@@ -39,6 +40,7 @@ void oracle_set_projection_poisson_params(const poisson_solver_params_t* p) {
     g_have_pparams = p != NULL;
     if (p) g_pparams = *p;
 }
+void oracle_set_gpu_rhs(int on) { g_gpu_rhs = on ? 1 : 0; }
 int oracle_get_threads(void) { return g_threads; }
 void oracle_last_phase_ms(double out[4]) { memcpy(out, g_phase_ms, sizeof(g_phase_ms)); }
 
@@ -218,6 +220,19 @@ void oracle_poisson_apply_bc(double* x, size_t nx, size_t ny, size_t nz) {
     for (size_t k = 0; k < nz; k++) oracle_bc_neumann_3d(x + k * plane, nx, ny, 1);
 }
 
+/* poisson_solver_apply_bc (linear_solver.c:348-359): the caller's apply_bc
+ * override when one is installed, else the default Neumann BC above */
+static oracle_bc_hook g_bc_hook = NULL;
+static void* g_bc_hook_ctx = NULL;
+void oracle_set_poisson_bc_hook(oracle_bc_hook fn, void* ctx) {
+    g_bc_hook = fn;
+    g_bc_hook_ctx = ctx;
+}
+static void solver_apply_bc(double* x, size_t nx, size_t ny, size_t nz) {
+    if (g_bc_hook) g_bc_hook(x, nx, ny, nz, g_bc_hook_ctx);
+    else oracle_poisson_apply_bc(x, nx, ny, nz);
+}
+
 /* ------------------------------------------------------------------------ */
 /* Poisson solvers                                                           */
 /* ------------------------------------------------------------------------ */
@@ -324,7 +339,7 @@ cfd_status_t oracle_cg_solve(double* x, const double* rhs, size_t nx, size_t ny,
     }
     double t0 = now_ms();
 
-    oracle_poisson_apply_bc(x, nx, ny, nz);                     /* cg.c:320 */
+    solver_apply_bc(x, nx, ny, nz);                             /* cg.c:320 */
     PAR                                                          /* cg.c:134-158 */
     for (size_t k = g.k0; k < g.k1; k++)
         for (size_t j = 1; j < ny - 1; j++)
@@ -409,7 +424,7 @@ cfd_status_t oracle_cg_solve(double* x, const double* rhs, size_t nx, size_t ny,
         rho = rho_new;
     }
     if (!converged && (res_norm < tolerance || res_norm < prm.absolute_tolerance)) converged = 1;
-    oracle_poisson_apply_bc(x, nx, ny, nz);                     /* cg.c:447 */
+    solver_apply_bc(x, nx, ny, nz);                             /* cg.c:447 */
     if (stats) {
         stats->iterations = (iter < prm.max_iterations) ? (iter + 1) : iter;
         stats->final_residual = res_norm;
@@ -591,7 +606,7 @@ static void redblack_sweep(void* vctx, double* x, double* xt, const double* rhs)
                 }
             }
     }
-    oracle_poisson_apply_bc(x, c->nx, c->ny, c->nz);
+    solver_apply_bc(x, c->nx, c->ny, c->nz);
 }
 
 cfd_status_t oracle_redblack_solve(double* x, const double* rhs, size_t nx, size_t ny, size_t nz,
@@ -619,7 +634,7 @@ static void jacobi_sweep(void* vctx, double* x, double* xt, const double* rhs) {
                           c->inv_factor;
             }
     memcpy(x, xt, c->nx * c->ny * c->nz * sizeof(double));
-    oracle_poisson_apply_bc(x, c->nx, c->ny, c->nz);
+    solver_apply_bc(x, c->nx, c->ny, c->nz);
 }
 
 cfd_status_t oracle_jacobi_solve(double* x, double* x_temp, const double* rhs, size_t nx,
@@ -921,7 +936,7 @@ cfd_status_t oracle_projection_step(flow_field* field, const grid* grid,
                 double dvs = (vs[idx + nx] - vs[idx - nx]) / (2.0 * dy);
                 double dws = (ws[idx + sz] - ws[idx - sz]) * inv_2dz;
                 double div = dus + dvs + dws;
-                rhs[idx] = (rho / dt) * div;
+                rhs[idx] = (g_gpu_rhs ? 1.0 / dt : rho / dt) * div;
             }
     double t2 = now_ms();
 

@@ -36,6 +36,15 @@ int oracle_get_threads(void);
  * (the reference always passes NULL = defaults, linear_solver.c:684); NULL
  * restores the defaults. Used to pair with a HIP context configured alike. */
 void oracle_set_projection_poisson_params(const poisson_solver_params_t* p);
+/* 1: the projection step's RHS is div(u*) / dt without rho, as the reference
+ * GPU computes it (solver_projection_gpu.cu:706-707); 0 (default): (rho / dt)
+ * div(u*), solver_projection.c:195-211. */
+void oracle_set_gpu_rhs(int on);
+/* A caller apply_bc override for the Poisson solvers (solver->apply_bc,
+ * linear_solver.c:356-359; test_poisson_3d.c:274): called wherever the
+ * reference calls poisson_solver_apply_bc. NULL restores the Neumann default. */
+typedef void (*oracle_bc_hook)(double* x, size_t nx, size_t ny, size_t nz, void* ctx);
+void oracle_set_poisson_bc_hook(oracle_bc_hook fn, void* ctx);
 
 /* grid.c:9-127 (grid_create + grid_initialize_uniform) */
 grid* oracle_grid_create_uniform(size_t nx, size_t ny, size_t nz, double xmin, double xmax,

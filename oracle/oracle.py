@@ -16,6 +16,9 @@ import numpy as np
 from cfd_amd import _abi as A
 
 ORACLE_DIR = Path(__file__).resolve().parent
+# void (*)(double* x, size_t nx, size_t ny, size_t nz, void* ctx)
+BC_HOOK = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_size_t, C.c_size_t, C.c_size_t,
+                      C.c_void_p)
 LIB = ORACLE_DIR / "build" / "liboracle.so"
 _lib = None
 
@@ -46,6 +49,8 @@ def lib():
         sig("oracle_get_threads", C.c_int)
         sig("oracle_set_poisson_cap", None, C.c_int)
         sig("oracle_set_projection_poisson_params", None, P(A.PoissonParams))
+        sig("oracle_set_gpu_rhs", None, C.c_int)
+        sig("oracle_set_poisson_bc_hook", None, BC_HOOK, C.c_void_p)
         sig("oracle_projection_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
             P(A.SolverStats), C.c_int, P(C.c_int))
         sig("oracle_last_phase_ms", None, d)

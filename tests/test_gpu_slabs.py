@@ -180,11 +180,12 @@ def test_slab_cg_cavity_vs_oracle(hip_lib, nranks):
         assert float(np.max(np.abs(got[k] - ref))) / scale <= 1e-10, k
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_slab_taylor_green_vs_oracle(hip_lib, nranks):
+@pytest.mark.parametrize("nranks,n", [(2, 17), (3, 17), (8, 33)])
+def test_slab_taylor_green_vs_oracle(hip_lib, nranks, n):
     """Config 4 at test size: periodic BCs across the slab boundary every step
-    (with 2 ranks both neighbours of each rank are the same peer)."""
-    g, f, p = cases.tg3(17)
+    (with 2 ranks both neighbours of each rank are the same peer; 8 ranks is
+    the configs[3] decomposition)."""
+    g, f, p = cases.tg3(n)
     S = Slabs(g, nranks)
     try:
         S.scatter(f)
