@@ -139,6 +139,8 @@ class HipProjConfig(C.Structure):
         ("verbose", C.c_int), ("sweep_rows", C.c_int), ("sweep_variant", C.c_int),
         ("rhs_density", C.c_int), ("poisson_fail_fatal", C.c_int), ("relax_two_pass", C.c_int),
         ("sweep_variant_fold", C.c_int),
+        ("dirty_faces", C.c_int),
+        ("dirty_sync_interval", C.c_int),
     ]
 
 

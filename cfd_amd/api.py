@@ -480,6 +480,11 @@ class HipProjection:
     def download(self, field: FlowField):
         _check(self._lib().hip_proj_download(self._ctx, field.ptr), "hip_proj_download")
 
+    def sync_host(self, field: FlowField):
+        """hip_proj_sync_host: the whole of u, v, w, p (T) to the host field
+        (the resident mode's full download)."""
+        _check(self._lib().hip_proj_sync_host(self._ctx, field.ptr), "hip_proj_sync_host")
+
     def step(self, field: FlowField, grid: Grid, params: A.SolverParams,
              stats: Optional[A.SolverStats] = None) -> int:
         st = stats if stats is not None else A.SolverStats()

@@ -401,6 +401,7 @@ cfd_status_t hip_proj_checkpoint_read(hip_proj_ctx_t* c, const char* path, grid*
         if (hipStreamSynchronize(c->stream) != hipSuccess) r.st = CFD_ERROR;
         c->rho0 = rho0;
         c->have_T = c->T_dirty = 1;
+        c->resident = 0;
     }
     for (int q = 0; q < CHK_NFIELDS; q += 2) scrub_scratch(c, dst[q], dst[q + 1]);
     if (r.st != CFD_SUCCESS) {

@@ -93,6 +93,16 @@ struct hip_proj_ctx {
     // every relaxation iteration the shell is copied from bcfix
     int poisson_bc = 0;
     double* bcfix = nullptr;
+    // resident mode of the host-buffer step (cfg.dirty_faces): the device
+    // fields equal the caller's host arrays res_ptr[] except in the cells the
+    // caller may have changed since (the boundary shell); any other entry
+    // that changes device state clears `resident`
+    int resident = 0;
+    const double* res_ptr[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    long long res_steps = 0;     // host steps since the last full download
+    double* shell_dev = nullptr;  // packed shell staging (device / pinned host)
+    double* shell_host = nullptr;
+    size_t shell_cap = 0;
     double* Tn = nullptr;  // energy equation output (swapped with T)
     double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated
     double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3
@@ -306,3 +316,10 @@ cfd_status_t ctx_validate_params(const hip_proj_ctx* c, const grid* g,
     __attribute__((visibility("hidden")));
 // compute_max_temperature into red[3] when T changed; call before reduce_red.
 void ctx_queue_max_T(hip_proj_ctx* c) __attribute__((visibility("hidden")));
+// Boundary-shell transfers (shell_io.hip): depth-`depth` shell of nf fields
+// between caller host arrays (nx*ny*nz) and device fields.
+bool ctx_shell_fits(const hip_proj_ctx* c, int depth) __attribute__((visibility("hidden")));
+cfd_status_t ctx_shell_put(hip_proj_ctx* c, const double* const* host, double* const* dev, int nf,
+                           int depth) __attribute__((visibility("hidden")));
+cfd_status_t ctx_shell_get(hip_proj_ctx* c, double* const* host, double* const* dev, int nf,
+                           int depth) __attribute__((visibility("hidden")));

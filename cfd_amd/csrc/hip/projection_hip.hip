@@ -582,6 +582,8 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.poisson_fail_fatal = 1;
     c.relax_two_pass = 0;
     c.sweep_variant_fold = 0;
+    c.dirty_faces = 0;
+    c.dirty_sync_interval = 0;
     return c;
 }
 
@@ -604,6 +606,8 @@ static void free_ctx(hip_proj_ctx* c) {
     if (c->dsum) hipFree(c->dsum);
     if (c->h_state) hipHostFree(c->h_state);
     if (c->h_red) hipHostFree(c->h_red);
+    if (c->shell_host) hipHostFree(c->shell_host);
+    if (c->shell_dev) hipFree(c->shell_dev);
     for (int i = 0; i < 2; i++)
         if (c->ev_poll[i]) hipEventDestroy(c->ev_poll[i]);
     for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -875,6 +879,7 @@ cfd_status_t hip_proj_set_field(hip_proj_ctx_t* c, int id, const double* host) {
         d = *slot;
     }
     if (!d) return CFD_ERROR_INVALID;
+    c->resident = 0;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpy2DAsync(d, c->px * sizeof(double), host, c->nx * sizeof(double),
                              c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
@@ -912,6 +917,7 @@ cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
         if (id == HIP_FIELD_T) c->have_T = 1;
     }
     if (!d) return CFD_ERROR_INVALID;
+    c->resident = 0;
     HIP_TRY(hipSetDevice(c->device));
     hipExtLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, c->stream, c->ta, c->tb, 0, d,
                        (long long)field_elems(c), value);
@@ -960,6 +966,7 @@ cfd_status_t hip_proj_download(hip_proj_ctx_t* c, flow_field* f) {
 
 cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type) {
     if (!c) return CFD_ERROR_INVALID;
+    c->resident = 0;
     double* d = field_ptr(c, id);
     if (!d) return CFD_ERROR_INVALID;
     int mode;
@@ -987,6 +994,7 @@ cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type)
 
 cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* c, int id, const bc_dirichlet_values_t* v) {
     if (!c || !v) return CFD_ERROR_INVALID;
+    c->resident = 0;
     double* d = field_ptr(c, id);
     if (!d) return CFD_ERROR_INVALID;
     DirVals dv{v->left, v->right, v->top, v->bottom, v->front, v->back};
@@ -998,6 +1006,7 @@ cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* c, int id, const bc_dirich
 
 cfd_status_t hip_proj_apply_thermal_bcs(hip_proj_ctx_t* c, const ns_solver_params_t* prm) {
     if (!c || !prm) return CFD_ERROR_INVALID;
+    c->resident = 0;
     if (!c->T) {
         set_err(CFD_ERROR_INVALID, "energy_apply_thermal_bcs: missing temperature field");
         return CFD_ERROR_INVALID;
@@ -1269,29 +1278,58 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
 
 cfd_status_t hip_proj_step_device(hip_proj_ctx_t* c, const grid* g,
                                   const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
+    if (c) c->resident = 0;
     return step_device_impl(c, g, prm, stats, 0);
 }
 
 }  // extern "C"
 
-// Host-buffer path shared by hip_proj_step (one step) and the plugin's solve
-// (n steps, source-term iteration index 0..n-1 as in solver_projection.c:112).
-extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter_internal(
-    hip_proj_ctx_t* c, flow_field* f, const grid* g, const ns_solver_params_t* prm,
-    ns_solver_stats_t* stats, int n_steps) {
+// Fields of the host-buffer step: u, v, w, p and, when present, T.
+static int host_fields(hip_proj_ctx* c, flow_field* f, double** host, double** dev) {
+    host[0] = f->u, host[1] = f->v, host[2] = f->w, host[3] = f->p;
+    dev[0] = c->u, dev[1] = c->v, dev[2] = c->w, dev[3] = c->p;
+    if (!f->T || !c->T) return 4;
+    host[4] = f->T;
+    dev[4] = c->T;
+    return 5;
+}
+
+// Host-buffer path shared by hip_proj_step (one step, shell_ok = 1) and the
+// plugin's solve (n steps, source-term iteration index 0..n-1 as in
+// solver_projection.c:112). In the resident mode (cfg.dirty_faces, see
+// shell_io.hip) a step on the same host arrays as the previous one uploads
+// only the depth-1 boundary shell and downloads the depth-2 shell.
+static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
+                               const ns_solver_params_t* prm, ns_solver_stats_t* stats,
+                               int n_steps, bool shell_ok) {
     if (!c || !f || !g || !prm) return CFD_ERROR_INVALID;
     if (f->nx < 3 || f->ny < 3 || (f->nz > 1 && f->nz < 3)) return CFD_ERROR_INVALID;
     cfd_status_t s = ctx_validate_params(c, g, prm);
     if (s != CFD_SUCCESS) return s;
     if (n_steps <= 0) return CFD_SUCCESS;
-    if ((s = hip_proj_set_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;
-    if ((s = hip_proj_set_field(c, HIP_FIELD_V, f->v)) != CFD_SUCCESS) return s;
-    if ((s = hip_proj_set_field(c, HIP_FIELD_W, f->w)) != CFD_SUCCESS) return s;
-    if ((s = hip_proj_set_field(c, HIP_FIELD_P, f->p)) != CFD_SUCCESS) return s;
     const bool need_T = (prm->beta != 0.0) || (prm->alpha > 0.0);
-    if (need_T && f->T) {
-        if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
+    const bool shell = shell_ok && c->cfg.dirty_faces > 0 && ctx_shell_fits(c, 2);
+    const bool same = c->resident && c->res_ptr[0] == f->u && c->res_ptr[1] == f->v &&
+                      c->res_ptr[2] == f->w && c->res_ptr[3] == f->p &&
+                      c->res_ptr[4] == f->T && (!f->T || c->T);
+    if (shell && same) {
+        double* host[5];
+        double* dev[5];
+        const int nf = host_fields(c, f, host, dev);
+        ST_TRY(ctx_shell_put(c, host, dev, nf, 1));
+        if (nf == 5) c->T_dirty = 1;
+    } else {
+        if ((s = hip_proj_set_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;
+        if ((s = hip_proj_set_field(c, HIP_FIELD_V, f->v)) != CFD_SUCCESS) return s;
+        if ((s = hip_proj_set_field(c, HIP_FIELD_W, f->w)) != CFD_SUCCESS) return s;
+        if ((s = hip_proj_set_field(c, HIP_FIELD_P, f->p)) != CFD_SUCCESS) return s;
+        // resident mode: T travels too, so its maximum comes from the device
+        if (f->T && (need_T || shell)) {
+            if ((s = hip_proj_set_field(c, HIP_FIELD_T, f->T)) != CFD_SUCCESS) return s;
+        }
+        c->res_steps = 0;
     }
+    c->resident = 0;
     c->rho0 = f->rho ? f->rho[0] : 1.0;
     int done = 0;  // steps completed: the reference leaves them applied to field
     for (int it = 0; it < n_steps; ++it) {
@@ -1301,15 +1339,35 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter
     }
     // a failed step (pressure solve unconverged, communication) leaves the
     // device u, v, w, p as the completed steps made them
+    const bool energy_T = prm->alpha > 0.0 && f->T && c->T;
     if (s == CFD_SUCCESS || s == CFD_ERROR_DIVERGED || done > 0) {
+        ++c->res_steps;
+        const int every = c->cfg.dirty_sync_interval;
+        if (shell && s == CFD_SUCCESS && !(every > 0 && c->res_steps % every == 0)) {
+            double* host[5];
+            double* dev[5];
+            const int nall = host_fields(c, f, host, dev);
+            ST_TRY(ctx_shell_get(c, host, dev, energy_T ? nall : 4, 2));
+        } else {
+            cfd_status_t d = hip_proj_download(c, f);
+            if (d != CFD_SUCCESS) return d;
+            if (energy_T) {
+                d = hip_proj_get_field(c, HIP_FIELD_T, f->T);
+                if (d != CFD_SUCCESS) return d;
+            }
+        }
+    } else if (shell) {
+        // nothing completed: the device holds the uploaded state; make the
+        // whole host field current before handing the error back
         cfd_status_t d = hip_proj_download(c, f);
         if (d != CFD_SUCCESS) return d;
-        if (prm->alpha > 0.0 && f->T && c->T) {
-            d = hip_proj_get_field(c, HIP_FIELD_T, f->T);
-            if (d != CFD_SUCCESS) return d;
-        }
     }
-    if (s == CFD_SUCCESS && stats && f->T) {
+    if (shell) {
+        c->resident = 1;
+        c->res_ptr[0] = f->u, c->res_ptr[1] = f->v, c->res_ptr[2] = f->w, c->res_ptr[3] = f->p;
+        c->res_ptr[4] = f->T;
+    }
+    if (s == CFD_SUCCESS && stats && f->T && !shell) {
         // compute_max_temperature (solver_registry.c:52-62) on the host copy
         size_t n = c->nx * c->ny * c->nz;
         double m = f->T[0];
@@ -1318,6 +1376,18 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter
         stats->max_temperature = m;
     }
     return s;
+}
+
+extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_iter_internal(
+    hip_proj_ctx_t* c, flow_field* f, const grid* g, const ns_solver_params_t* prm,
+    ns_solver_stats_t* stats, int n_steps) {
+    return host_steps(c, f, g, prm, stats, n_steps, false);
+}
+
+extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_proj_step_host_internal(
+    hip_proj_ctx_t* c, flow_field* f, const grid* g, const ns_solver_params_t* prm,
+    ns_solver_stats_t* stats) {
+    return host_steps(c, f, g, prm, stats, 1, true);
 }
 
 extern "C" __attribute__((visibility("hidden"))) int hip_proj_matches_internal(const hip_proj_ctx_t* c,
@@ -1330,7 +1400,16 @@ extern "C" {
 
 cfd_status_t hip_proj_step(hip_proj_ctx_t* c, flow_field* f, const grid* g,
                            const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
-    return hip_proj_step_iter_internal(c, f, g, prm, stats, 1);
+    return host_steps(c, f, g, prm, stats, 1, true);
+}
+
+cfd_status_t hip_proj_sync_host(hip_proj_ctx_t* c, flow_field* f) {
+    if (!c || !f) return CFD_ERROR_INVALID;
+    if (f->nx != c->nx || f->ny != c->ny || f->nz != c->nz) return CFD_ERROR_INVALID;
+    ST_TRY(hip_proj_download(c, f));
+    if (c->resident && f->T && c->T) ST_TRY(hip_proj_get_field(c, HIP_FIELD_T, f->T));
+    c->res_steps = 0;
+    return CFD_SUCCESS;
 }
 
 cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* c, int method, double* x, const double* rhs,
@@ -1351,6 +1430,7 @@ cfd_status_t hip_proj_poisson_solve_ex(hip_proj_ctx_t* c, int method, double* x,
                                        const poisson_solver_params_t* params,
                                        poisson_solver_stats_t* stats, int bc_mode,
                                        const double* bc_values) {
+    if (c) c->resident = 0;  // the solve reuses the step's pressure buffers
     if (!c || !x || !rhs) return CFD_ERROR_INVALID;
     if (bc_mode != HIP_POISSON_BC_NEUMANN && bc_mode != HIP_POISSON_BC_NONE &&
         bc_mode != HIP_POISSON_BC_FIXED)

@@ -157,6 +157,7 @@ extern "C" __attribute__((visibility("hidden"))) cfd_status_t hip_rk4_step_iter_
     if (f->nx < 3 || f->ny < 3 || (f->nz > 1 && f->nz < 3)) return CFD_ERROR_INVALID;
     ST_TRY(ctx_validate_params(c, g, prm));
     if (n_steps <= 0) return CFD_SUCCESS;
+    c->resident = 0;
     const int ids[4] = {HIP_FIELD_U, HIP_FIELD_V, HIP_FIELD_W, HIP_FIELD_P};
     double* hf[4] = {f->u, f->v, f->w, f->p};
     for (int q = 0; q < 4; ++q) ST_TRY(hip_proj_set_field(c, ids[q], hf[q]));

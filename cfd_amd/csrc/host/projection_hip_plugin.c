@@ -27,6 +27,10 @@ CFD_HIP_INTERNAL cfd_status_t hip_proj_step_iter_internal(hip_proj_ctx_t* ctx, f
                                                           const grid* g,
                                                           const ns_solver_params_t* params,
                                                           ns_solver_stats_t* stats, int n_steps);
+CFD_HIP_INTERNAL cfd_status_t hip_proj_step_host_internal(hip_proj_ctx_t* ctx, flow_field* field,
+                                                          const grid* g,
+                                                          const ns_solver_params_t* params,
+                                                          ns_solver_stats_t* stats);
 CFD_HIP_INTERNAL cfd_status_t hip_rk4_step_iter_internal(hip_proj_ctx_t* ctx, flow_field* field,
                                                          const grid* g,
                                                          const ns_solver_params_t* params,
@@ -67,6 +71,14 @@ static cfd_status_t get_ctx(ns_solver_t* solver, const grid* g, hip_proj_ctx_t**
         hip_proj_config_t cfg = hip_proj_config_default();
         cfg.poisson_method = method_of(solver);
         if (cfg.poisson_method == HIP_POISSON_JACOBI) cfg.poisson_max_iter = 2000; /* linear_solver.c:274-276 */
+        /* CFD_HIP_DIRTY_FACES=N: the resident mode of `step` with a full
+         * download every N steps (the driver's output interval), see
+         * hip_proj_config_t.dirty_faces; the reference API has no other way in */
+        const char* e = getenv("CFD_HIP_DIRTY_FACES");
+        if (e && atoi(e) > 0) {
+            cfg.dirty_faces = 1;
+            cfg.dirty_sync_interval = atoi(e);
+        }
         pc->ctx = hip_proj_create(g->nx, g->ny, g->nz, &cfg);
         if (!pc->ctx) return CFD_ERROR_UNSUPPORTED;
     }
@@ -111,6 +123,7 @@ static cfd_status_t plugin_step(ns_solver_t* solver, flow_field* field, const gr
     hip_proj_ctx_t* ctx = NULL;
     cfd_status_t s = get_ctx(solver, g, &ctx);
     if (s != CFD_SUCCESS) return s;
+    if (!is_rk4(solver)) return hip_proj_step_host_internal(ctx, field, g, params, stats);
     return run_steps(solver, ctx, field, g, params, stats, 1);
 }
 

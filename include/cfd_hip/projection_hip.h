@@ -83,6 +83,22 @@ typedef struct {
                                      the two colour sweeps */
     int sweep_variant_fold;       /* memory hints of the x-folding sweep B (every 4th CG
                                      iteration, 16-row tiles): 0 = sweep_variant; 3, 11, 15 */
+    int dirty_faces;              /* host-buffer step (hip_proj_step, the plugin's `step`):
+                                     0 = upload and download u, v, w, p (T) in full every
+                                     step (default); 1 = resident mode: the interior stays in
+                                     HBM between steps on the same host arrays, a step uploads
+                                     only the boundary shell (the cells a caller's BC routine
+                                     writes) and downloads the two outer layers (what it
+                                     reads). The rest of the host arrays is refreshed by
+                                     hip_proj_sync_host, every dirty_sync_interval steps, and
+                                     after a failed step. Any other entry that changes device
+                                     state (set_field, fill, BCs, step_device, poisson_solve,
+                                     checkpoint_read, RK4) or new host arrays end the resident
+                                     run: the next step uploads the host arrays in full, so
+                                     call hip_proj_sync_host before such an entry when the
+                                     same host arrays go on. Single-device contexts. */
+    int dirty_sync_interval;      /* resident mode: full download every N-th step (0 = only
+                                     on hip_proj_sync_host / failure) */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
@@ -129,6 +145,11 @@ CFD_HIP_EXPORT void hip_proj_destroy(hip_proj_ctx_t* ctx);
 CFD_HIP_EXPORT cfd_status_t hip_proj_step(hip_proj_ctx_t* ctx, flow_field* field, const grid* g,
                                           const ns_solver_params_t* params,
                                           ns_solver_stats_t* stats);
+
+/* Resident mode (cfg.dirty_faces): copy the whole of u, v, w, p (and T when
+ * resident) to the caller's field, so that every host cell is current. A
+ * no-op copy of the full fields otherwise. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_sync_host(hip_proj_ctx_t* ctx, flow_field* field);
 
 /* Device-resident path. */
 CFD_HIP_EXPORT cfd_status_t hip_proj_upload(hip_proj_ctx_t* ctx, const flow_field* field);

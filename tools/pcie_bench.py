@@ -4,7 +4,11 @@ u, v, w, p from the caller's flow_field, one step, download u, v, w, p --
 the path the projection_hip plugin's `step` takes) against the
 HBM-resident step (hip_proj_step_device) at N^3 (default 512^3, BASELINE
 configs[2]), and the field copy rate from pageable and from pinned host
-memory. One JSON line.
+memory. Then the same STEPS-step cavity run (lid BC re-applied on the host
+before each step) through the full-transfer step and through the resident
+mode (dirty_faces = 1): the two runs do identical work (same CG iterations,
+bitwise-equal results), so the wall-time difference is the transfer saved.
+One JSON line.
 
 usage: N=512 python tools/pcie_bench.py
 """
@@ -71,6 +75,38 @@ def main():
     it_host = ctx.poisson_stats().iterations
     ctx.close()
     cells = (n - 2) ** 3
+    steps = int(os.environ.get("STEPS", "3"))
+    runs = {}
+    for mode in (0, 1):
+        g, f, p = cases.cavity(n, n, n, Re=1000.0, dt=1e-4)
+        c = api.HipProjection(n, n, n, dirty_faces=mode)
+        walls, its = [], []
+        for _ in range(steps):
+            api.cavity_bc(f, 1.0)
+            t0 = time.perf_counter()
+            assert c.step(f, g, p) == A.CFD_SUCCESS, _native.last_error()
+            walls.append(time.perf_counter() - t0)
+            its.append(c.poisson_stats().iterations)
+        t0 = time.perf_counter()
+        c.sync_host(f)
+        t_sync = time.perf_counter() - t0
+        c.close()
+        runs[mode] = (walls, its, t_sync, f)
+    (wf, itf, _, ff), (wr, itr, t_sync, fr) = runs[0], runs[1]
+    assert itf == itr, (itf, itr)
+    same = all(np.array_equal(getattr(ff, k), getattr(fr, k)) for k in ("u", "v", "w", "p"))
+    ss = slice(1, None)  # steady state: the resident run's first step uploads in full
+    mean = lambda a: sum(a[ss]) / len(a[ss])
+    out["cavity_run"] = {
+        "steps": steps, "cg_iters": itf, "bitwise_equal_after_sync": same,
+        "full_transfer_ms": [round(x * 1e3, 2) for x in wf],
+        "resident_ms": [round(x * 1e3, 2) for x in wr],
+        "sync_host_ms": round(t_sync * 1e3, 2),
+        "full_transfer_MLUPS": [round(cells / x / 1e6, 2) for x in wf],
+        "resident_MLUPS": [round(cells / x / 1e6, 2) for x in wr],
+        "full_transfer_MLUPS_steady": round(cells / mean(wf) / 1e6, 2),
+        "resident_MLUPS_steady": round(cells / mean(wr) / 1e6, 2),
+        "saved_ms_per_step": round((mean(wf) - mean(wr)) * 1e3, 2)}
     out.update({
         "step_device_ms": round(t_dev * 1e3, 2), "step_device_cg_iters": it_dev,
         "step_device_MLUPS": round(cells / t_dev / 1e6, 2),
