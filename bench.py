@@ -35,6 +35,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
 BYTES_SWEEP_B = 24.0    # non-fold iterations: read p, r; write r
 BYTES_SWEEP_BX = 64.0   # every 4th iteration: + read x, p_{it-3..it-1}; write x (4 alpha p folded)
+BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
+BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
 BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
 
@@ -61,6 +63,12 @@ def parse():
     ap.add_argument("--sweep-variant", type=int, default=15,
                     help="CG sweep variant: bit0 NT stores, bit1 NT loads, bit2 plane prefetch "
                          "(built: 0-4, 7)")
+    ap.add_argument("--cg-variant", type=int, default=0, choices=(0, 1),
+                    help="0: textbook CG (the reference's loop); 1: single-reduction "
+                         "(Chronopoulos-Gear) CG")
+    ap.add_argument("--no-compare-cg-variant", action="store_true",
+                    help="skip the side measurement of the other CG variant after the "
+                         "timed region")
     return ap.parse_args()
 
 
@@ -108,27 +116,32 @@ def main():
         uid = [api.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = api.SlabComm.rccl(uid[0], rank, world, local)
-    ctx = api.HipProjection(n, n, n, comm=comm, device=local, kchunk=args.kchunk,
-                             sweep_rows=args.sweep_rows, sweep_variant=args.sweep_variant)
-    for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
-        ctx.fill(fid, 0.0)
-    ctx.set_density(1.0)
-    if tg:
-        import numpy as np
-        x = np.asarray(g.x)
-        z = np.asarray(g.z)[ctx.k_offset:ctx.k_offset + ctx.nz_local]
-        cz = np.cos(z)[:, None, None]
-        ctx.set_field(A.HIP_FIELD_U, np.cos(x)[None, None, :] * np.sin(x)[None, :, None] * cz)
-        ctx.set_field(A.HIP_FIELD_V, -np.sin(x)[None, None, :] * np.cos(x)[None, :, None] * cz)
-    else:
-        # caller BCs (lid_driven_cavity_common.h:142-148, 3-D form): u = 1 on the
-        # lid; the step preserves boundary faces, so applying them once is the
-        # same as before every step
-        ctx.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
-        ctx.apply_dirichlet(A.HIP_FIELD_V, api.dirichlet())
-        ctx.apply_dirichlet(A.HIP_FIELD_W, api.dirichlet())
-        ctx.apply_scalar_bc(A.HIP_FIELD_P, A.BC_TYPE_NEUMANN)
-    ctx.synchronize()
+    def make_ctx(cg_variant):
+        c = api.HipProjection(n, n, n, comm=comm, device=local, kchunk=args.kchunk,
+                              sweep_rows=args.sweep_rows, sweep_variant=args.sweep_variant,
+                              cg_variant=cg_variant)
+        for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
+            c.fill(fid, 0.0)
+        c.set_density(1.0)
+        if tg:
+            import numpy as np
+            x = np.asarray(g.x)
+            z = np.asarray(g.z)[c.k_offset:c.k_offset + c.nz_local]
+            cz = np.cos(z)[:, None, None]
+            c.set_field(A.HIP_FIELD_U, np.cos(x)[None, None, :] * np.sin(x)[None, :, None] * cz)
+            c.set_field(A.HIP_FIELD_V, -np.sin(x)[None, None, :] * np.cos(x)[None, :, None] * cz)
+        else:
+            # caller BCs (lid_driven_cavity_common.h:142-148, 3-D form): u = 1 on
+            # the lid; the step preserves boundary faces, so applying them once
+            # is the same as before every step
+            c.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
+            c.apply_dirichlet(A.HIP_FIELD_V, api.dirichlet())
+            c.apply_dirichlet(A.HIP_FIELD_W, api.dirichlet())
+            c.apply_scalar_bc(A.HIP_FIELD_P, A.BC_TYPE_NEUMANN)
+        c.synchronize()
+        return c
+
+    ctx = make_ctx(args.cg_variant)
 
     def step():
         if tg:  # periodic BCs on u, v, w, p before every step (collective on slabs)
@@ -176,22 +189,29 @@ def main():
     kt = ctx.timing()
     dflag = "true" if world > 1 else "false"
     sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s, total ms)
-    for key, kname, bpc in (
+    if args.cg_variant == 1:
+        sweep_set = (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
+                     ("cc_spmv", f"k_cc2<{args.sweep_rows}, {dflag}, false>", BYTES_CC_SPMV))
+    else:
+        sweep_set = (
             ("cg_sweep_a", f"k_cgA<{args.sweep_rows}, false, {dflag}, {args.sweep_variant}>",
              BYTES_SWEEP_A),
             ("cg_sweep_b", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, false>",
              BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, true>",
-             BYTES_SWEEP_BX)):
+             BYTES_SWEEP_BX))
+    for key, kname, bpc in sweep_set:
         ms, cnt = kt[key]
         avg = ms / cnt if cnt else None
         ach = bpc * n_loc / (avg * 1e-3) / 1e9 if cnt else None
         sweeps[key] = (kname, bpc, avg, cnt, ach, ms)
-    # one CG iteration = sweep A + the mean of the two sweep B forms
-    avg_a = sweeps["cg_sweep_a"][2] or 0.0
-    nb = sweeps["cg_sweep_b"][3] + sweeps["cg_sweep_bx"][3]
-    avg_b = (sweeps["cg_sweep_b"][5] + sweeps["cg_sweep_bx"][5]) / nb if nb else 0.0
-    cg_iter_ms = avg_a + avg_b
+    if args.cg_variant == 1:  # one iteration = update + SpMV
+        cg_iter_ms = (sweeps["cc_update"][2] or 0.0) + (sweeps["cc_spmv"][2] or 0.0)
+    else:  # one CG iteration = sweep A + the mean of the two sweep B forms
+        avg_a = sweeps["cg_sweep_a"][2] or 0.0
+        nb = sweeps["cg_sweep_b"][3] + sweeps["cg_sweep_bx"][3]
+        avg_b = (sweeps["cg_sweep_b"][5] + sweeps["cg_sweep_bx"][5]) / nb if nb else 0.0
+        cg_iter_ms = avg_a + avg_b
     # roofline on the dominant sweep (largest total time)
     dom = max(sweeps, key=lambda k: sweeps[k][5])
     kname, bpc_dom, avg_dom, _, ach_dom, _ = sweeps[dom]
@@ -224,12 +244,49 @@ def main():
         cg.value = tr.value = 0.0
 
     ranks = None
+    tot_iters = max(1, sum(iters))
     if world > 1:  # per-rank device times, so the driver's 1 -> N curve can be read
+        per_it = lambda key: round(kt[key][0] / tot_iters, 4) if kt[key][1] else None
         mine = {"rank": rank, "planes": ctx.nz_local - 2,
                 "sweep_ms_per_iter": round(cg_iter_ms, 4),
+                "halo_ms_per_iter": per_it("halo"),
+                # with the device mailbox the all-reduce runs inside the sweeps
+                "allreduce_ms_per_iter": per_it("allreduce"),
+                "dot_allreduce": "mailbox (in sweep)" if comm.device_allreduce else "ncclAllReduce",
                 "timers_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
+
+    # side measurement of the other CG variant (same grid, ranks and stepping
+    # from the same initial state), after the timed region: per CG iteration,
+    # since its iteration counts differ from the main run's by rounding
+    other = None
+    if not args.no_compare_cg_variant:
+        ctx.close()
+        ctx = make_ctx(1 - args.cg_variant)
+        step()
+        ctx.synchronize()
+        ctx.reset_timing()
+        ctx.enable_timing(True)
+        if world > 1:
+            dist.barrier()
+        ta = time.perf_counter()
+        it2 = step()
+        ctx.synchronize()
+        tb = time.perf_counter()
+        ctx.enable_timing(False)
+        e2 = tb - ta
+        if world > 1:
+            tt = torch.tensor([e2], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            e2 = float(tt[0])
+        k2 = ctx.timing()
+        per2 = lambda key: round(k2[key][0] / max(1, it2), 4) if k2[key][1] else None
+        other = {"cg_variant": 1 - args.cg_variant, "step": args.warmup + 1,
+                 "cg_iters": it2, "ms_step": round(e2 * 1e3, 3),
+                 "ms_per_cg_iter_wall": round(e2 * 1e3 / max(1, it2), 4),
+                 "kernel_ms_per_iter": {k: per2(k) for k in k2 if k2[k][1]},
+                 "main_ms_per_cg_iter_wall": round(elapsed * 1e3 / tot_iters, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
@@ -282,6 +339,8 @@ def main():
                               "achieved_GBps": round(v[4], 1) if v[4] else None}
                           for k, v in sweeps.items()},
             "ranks": ranks,
+            "cg_variant": args.cg_variant,
+            "cg_variant_compare": other,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
@@ -293,7 +352,7 @@ def main():
 
 
 # timer -> kernel symbol in the PMC profile (the CG sweeps are named per variant)
-TIMER_KERNEL = {"predictor": "k_predictor<false>", "corrector": "k_corrector",
+TIMER_KERNEL = {"predictor": "k_pred2<false, 0>", "corrector": "k_corr2<0>",
                 "cg_setup": "k_cg_setup<true, false, true, false>"}
 
 

@@ -103,6 +103,7 @@ struct hip_proj_ctx {
     double* shell_dev = nullptr;  // packed shell staging (device / pinned host)
     double* shell_host = nullptr;
     size_t shell_cap = 0;
+    double *cw = nullptr, *cs = nullptr;  // cg_variant 1: w = A r, s = A p (lazily allocated)
     double* Tn = nullptr;  // energy equation output (swapped with T)
     double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated
     double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3
@@ -212,6 +213,19 @@ static void timed(hip_proj_ctx* c, int kind, F&& launch, int iter = -1) {
     launch();
     c->ta = c->tb = nullptr;
     c->pending.push_back({a, b, kind, iter});
+}
+
+// Time a span of stream work that is not one kernel (RCCL calls, halo
+// copies) with events recorded around it on stream `s`.
+template <typename F>
+static cfd_status_t timed_span(hip_proj_ctx* c, hipStream_t s, int kind, F&& fn, int iter = -1) {
+    if (!c->timing) return fn();
+    hipEvent_t a = take_event(c), b = take_event(c);
+    if (!a || !b) return fn();
+    if (hipEventRecord(a, s) != hipSuccess) return fn();
+    cfd_status_t r = fn();
+    if (hipEventRecord(b, s) == hipSuccess) c->pending.push_back({a, b, kind, iter});
+    return r;
 }
 
 static int tile_grid(const hip_proj_ctx* c) {

@@ -819,6 +819,265 @@ static __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, PRing pr,
     }
 }
 
+// ===========================================================================
+// Chronopoulos-Gear CG (opt-in, hip_proj_config_t.cg_variant = 1): the two
+// dot products of an iteration come out of ONE reduction, so a Z-slab run
+// needs one all-reduce per iteration instead of two. With
+// w = A r and s = A p kept as vectors (Chronopoulos & Gear 1989):
+//   p_i = r_i + beta_i p_{i-1},  s_i = w_i + beta_i s_{i-1}      (k_cc1)
+//   x_{i+1} = x_i + alpha_i p_i, r_{i+1} = r_i - alpha_i s_i      (k_cc1)
+//   w_{i+1} = A r_{i+1}; gamma = (r, r), delta = (w, r)          (k_cc2)
+//   beta_{i+1} = gamma_{i+1} / gamma_i,
+//   alpha_{i+1} = gamma_{i+1} / (delta_{i+1} - beta_{i+1} gamma_{i+1} / alpha_i)
+// Same operator, boundary semantics (zero walls in r, lagged Neumann x),
+// stopping rule and statistics as the textbook loop; the iterates differ by
+// rounding, so it is gated against textbook CG (iterations +-2, residual),
+// not bitwise. x += alpha p is folded every CG_XFOLD iterations as in k_cgB.
+// ===========================================================================
+// after the first w = A r_0: alpha_0 = (r,r) / (w,r) (the textbook's first
+// (p, Ap) with p_0 = r_0), breakdown as fin_A
+__device__ __forceinline__ void fin_cc0(CgState* st, double delta) {
+    st->pAp = delta;
+    if (fabs(delta) < 1e-30) {
+        st->done = 1;
+        st->status = ST_STAGNATED;
+        st->iterations = 1;
+    } else {
+        st->alpha[0] = st->rho / delta;
+        st->beta = 0.0;
+    }
+}
+
+// after iteration it's reduction: convergence test as fin_B, then beta and
+// the next alpha (its denominator standing in for the textbook's (p, Ap))
+__device__ __forceinline__ void fin_cc(CgState* st, double gamma, double delta, int it,
+                                       bool fold) {
+    if (fold) st->xdone = it + 1;
+    st->nalpha = it + 1;
+    const double res = sqrt(gamma);
+    st->res = res;
+    st->iterations = it + 1;
+    const bool check = (it % st->check_interval) == 0;
+    const bool conv = (res < st->tol) || (res < st->abs_tol);
+    if (check && conv) {
+        st->done = 1;
+        st->status = ST_CONVERGED;
+    } else if (fabs(st->rho) < 1e-30) {
+        st->done = 1;
+        st->status = ST_STAGNATED;
+    } else {
+        const double beta = gamma / st->rho;
+        const double den = delta - beta * gamma / st->alpha[it % CG_XFOLD];
+        st->beta = beta;
+        st->rho = gamma;
+        st->pAp = den;
+        if (it + 1 >= st->max_iter) {
+            st->done = 1;
+            st->status = conv ? ST_CONVERGED : ST_MAX_ITER;
+        } else if (fabs(den) < 1e-30) {
+            st->done = 1;
+            st->status = ST_STAGNATED;
+            st->iterations = it + 2;
+        } else {
+            st->alpha[(it + 1) % CG_XFOLD] = gamma / den;
+        }
+    }
+}
+
+static __global__ void k_finish_cc(CgState* st, const double* tot, int it, int fold, int init) {
+    if (threadIdx.x != 0 || st->done) return;
+    if (init) fin_cc0(st, tot[1]);
+    else fin_cc(st, tot[0], tot[1], it, fold != 0);
+}
+
+// Pointwise part of iteration it over the interior cells, 16-B pairs:
+// p_it into the ring slot pn, s in place, r in place; FOLD (it % 4 == 3)
+// also x += the four pending alpha_j p_j in the reference's order.
+template <bool FIRST, bool FOLD>
+static __global__ __launch_bounds__(256) void k_cc1(SGeo g, double* __restrict__ r,
+                                                    const double* __restrict__ w,
+                                                    double* __restrict__ s,
+                                                    const double* __restrict__ po,
+                                                    double* __restrict__ pn, PPrev pv,
+                                                    double* __restrict__ x, const CgState* st,
+                                                    int it) {
+    if (st->done) return;
+    const double a = st->alpha[it % CG_XFOLD];
+    const double ma = -a;
+    const double beta = FIRST ? 0.0 : st->beta;
+    double aq[CG_XFOLD - 1];
+#pragma unroll
+    for (int q = 0; q < CG_XFOLD - 1; ++q)
+        aq[q] = FOLD ? st->alpha[(it + 1 + q) % CG_XFOLD] : 0.0;  // alpha_{it-3+q}
+    const unsigned pairs = (unsigned)(g.px / 2);
+    const unsigned nyi = (unsigned)(g.ny - 2);
+    const unsigned n = pairs * nyi * (unsigned)(g.k1 - g.k0);
+    for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const unsigned row = e / pairs;
+        const int i0 = 2 * (int)(e - row * pairs);
+        if (i0 >= g.nx) continue;
+        const int j = 1 + (int)(row % nyi);
+        const int k = g.k0 + (int)(row / nyi);
+        const bool in0 = i0 >= 1 && i0 <= g.nx - 2;
+        const bool in1 = i0 + 1 <= g.nx - 2;
+        const long long idx = (long long)k * g.ps + (long long)j * g.px + i0;
+        const double2 rv = ld2(r, idx);
+        const double2 wv = ld2(w, idx);
+        const double2 pf = FIRST ? rv : fma2p(rv, beta, ld2(po, idx));
+        const double2 sf = FIRST ? wv : fma2p(wv, beta, ld2(s, idx));
+        const double2 pw = make_double2(in0 ? pf.x : 0.0, in1 ? pf.y : 0.0);
+        const double2 sw = make_double2(in0 ? sf.x : 0.0, in1 ? sf.y : 0.0);
+        st2(pn, idx, pw);
+        st2(s, idx, sw);
+        st2(r, idx, make_double2(in0 ? rv.x + ma * sf.x : rv.x, in1 ? rv.y + ma * sf.y : rv.y));
+        if (FOLD) {
+            const double2 xo = ld2(x, idx);
+            const double2 qa = ld2(pv.q[0], idx), qb = ld2(pv.q[1], idx), qc = ld2(pv.q[2], idx);
+            double2 xw;
+            xw.x = in0 ? (((xo.x + aq[0] * qa.x) + aq[1] * qb.x) + aq[2] * qc.x) + a * pf.x : xo.x;
+            xw.y = in1 ? (((xo.y + aq[0] * qa.y) + aq[1] * qb.y) + aq[2] * qc.y) + a * pf.y : xo.y;
+            st2(x, idx, xw);
+        }
+    }
+}
+
+// Two-value form of grid_sum_last_n (partials[b] and partials[gridDim.x + b]).
+template <int NTH>
+__device__ __forceinline__ bool grid_sum2_last(double b0, double b1, double* partials,
+                                               unsigned* counter, double* sh, int* flag,
+                                               double& t0, double& t1) {
+    const unsigned nb = gridDim.x;
+    if (threadIdx.x == 0) {
+        store_sc1(&partials[blockIdx.x], b0);
+        store_sc1(&partials[nb + blockIdx.x], b1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        *flag = (t == nb - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (*flag == 0) return false;
+    double s0 = 0.0, s1 = 0.0;
+    for (unsigned b = threadIdx.x; b < nb; b += NTH) {
+        s0 += load_sc1(&partials[b]);
+        s1 += load_sc1(&partials[nb + b]);
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if ((threadIdx.x & 63) == 0) {
+        sh[threadIdx.x >> 6] = s0;
+        sh[NTH / 64 + (threadIdx.x >> 6)] = s1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int q = 0; q < NTH / 64; ++q) {
+            a0 += sh[q];
+            a1 += sh[NTH / 64 + q];
+        }
+        t0 = a0;
+        t1 = a1;
+        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
+// w = A r on the row-pair tiling (k_cgA's stencil with p = r), written to w,
+// and the one reduction of iteration it: gamma = (r, r), delta = (w, r).
+// INIT: the w = A r_0 before iteration 0 (fin_cc0; gamma_0 comes from setup).
+template <int TY, bool DIST, bool INIT>
+static __global__ __launch_bounds__(64 * TY) void k_cc2(SGeo g, Lap L,
+                                                        const double* __restrict__ r,
+                                                        double* __restrict__ w, CgState* st,
+                                                        double* partials, unsigned* counter,
+                                                        int it, double* dsum, Mbox* mb) {
+    __shared__ double2 rows[2][TY + 2][64];
+    __shared__ double sh[2 * TY];
+    __shared__ int flag;
+    if (st->done) return;
+    RowPair c = row_pair<TY>(g);
+    const bool halo = (c.w == 0) || (c.w == TY - 1);
+    const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
+    const int hslot = (c.w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - min(c.j, g.ny - 1)) * g.px;
+    const bool xok = c.i0 < g.nx;
+    const bool eok_l = c.lane == 0 && c.i0 >= 1 && xok;
+    const bool eok_r = c.lane == 63 && c.i0 + 2 < g.nx;
+    const double2 zero = make_double2(0.0, 0.0);
+    double accg = 0.0, accd = 0.0;
+    long long idx = c.idx;
+    double2 pm = xok ? ld2(r, idx - g.sz) : zero;
+    double2 pc = xok ? ld2(r, idx) : zero;
+    double2 hc = (xok && halo) ? ld2(r, idx + hoff) : zero;
+    int buf = 0;
+    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        const long long ip = idx + g.sz;
+        const double2 pp = xok ? ld2(r, ip) : zero;
+        const double2 hn = (xok && halo && k + 1 < c.ke) ? ld2(r, ip + hoff) : zero;
+        const double el = eok_l ? r[idx - 1] : 0.0;
+        const double er = eok_r ? r[idx + 2] : 0.0;
+        rows[buf][c.w + 1][c.lane] = pc;
+        if (halo) rows[buf][hslot][c.lane] = hc;
+        __syncthreads();
+        const double2 ys = rows[buf][c.w][c.lane];
+        const double2 yn = rows[buf][c.w + 2][c.lane];
+        double left = __shfl_up(pc.y, 1, 64);
+        double right = __shfl_down(pc.x, 1, 64);
+        if (c.lane == 0) left = el;
+        if (c.lane == 63) right = er;
+        const double w0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
+        const double w1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
+        if (c.act) st2(w, idx, make_double2(c.in0 ? w0 : 0.0, c.in1 ? w1 : 0.0));
+        if (c.in0) {
+            accg += pc.x * pc.x;
+            accd += w0 * pc.x;
+        }
+        if (c.in1) {
+            accg += pc.y * pc.y;
+            accd += w1 * pc.y;
+        }
+        pm = pc;
+        pc = pp;
+        hc = hn;
+        buf ^= 1;
+    }
+    accg = wave_sum(accg);
+    accd = wave_sum(accd);
+    if (c.lane == 0) {
+        sh[c.w] = accg;
+        sh[TY + c.w] = accd;
+    }
+    __syncthreads();
+    double bg = 0.0, bd = 0.0;
+    if (threadIdx.x == 0)
+        for (int q = 0; q < TY; ++q) {
+            bg += sh[q];
+            bd += sh[TY + q];
+        }
+    double tg, td;
+    double* shs = (double*)&rows[0][0][0];
+    if (grid_sum2_last<64 * TY>(bg, bd, partials, counter, shs, &flag, tg, td) &&
+        threadIdx.x == 0) {
+        if (DIST && mb) {
+            double gg, gd;
+            if (mbox_allreduce2(mb, tg, td, &gg, &gd)) {
+                if (INIT) fin_cc0(st, gd);
+                else fin_cc(st, gg, gd, it, (it % CG_XFOLD) == CG_XFOLD - 1);
+            } else {
+                comm_fail(st);
+            }
+        } else if (DIST) {
+            dsum[0] = tg;
+            dsum[1] = td;
+        } else if (INIT) {
+            fin_cc0(st, td);
+        } else {
+            fin_cc(st, tg, td, it, (it % CG_XFOLD) == CG_XFOLD - 1);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Boundary conditions as pure gathers from interior cells (race-free):
 //   Neumann  (boundary_conditions_core_impl.h:41-85): c -> clamp(c, 1, n-2)

@@ -55,4 +55,41 @@ __device__ __forceinline__ bool mbox_allreduce(Mbox* mb, double v, double* out,
     return true;
 }
 
+// Two values in one exchange (the single-reduction CG's gamma and delta):
+// slots [v0, v1, seq] in a second region of the mailbox, same sequence
+// counter (so this and mbox_allreduce alternate parity consistently).
+constexpr int MBOX2_BASE = 128;  // u64 offset; the one-value region ends at 64
+__device__ __forceinline__ bool mbox_allreduce2(Mbox* mb, double v0, double v1, double* out0,
+                                                double* out1) {
+    const unsigned long long seq = mb->count + 1;
+    mb->count = seq;
+    const int n = mb->n, me = mb->rank;
+    const int par = (int)(seq & 1ull);
+    const unsigned long long b0 = (unsigned long long)__double_as_longlong(v0);
+    const unsigned long long b1 = (unsigned long long)__double_as_longlong(v1);
+    for (int r = 0; r < n; ++r) {
+        unsigned long long* s = mb->slot[r] + MBOX2_BASE + 3 * (par * MBOX_MAX + me);
+        __hip_atomic_store(s, b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(s + 1, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(s + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    unsigned long long* mine = mb->slot[me];
+    const long long t0 = wall_clock64();
+    double a0 = 0.0, a1 = 0.0;
+    for (int r = 0; r < n; ++r) {
+        unsigned long long* s = mine + MBOX2_BASE + 3 * (par * MBOX_MAX + r);
+        while (__hip_atomic_load(s + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > mb->timeout_ticks) return false;
+        }
+        a0 += __longlong_as_double(
+            (long long)__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        a1 += __longlong_as_double(
+            (long long)__hip_atomic_load(s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    *out0 = a0;
+    *out1 = a1;
+    return true;
+}
+
 }  // namespace cfdhip

@@ -120,6 +120,44 @@ static void launch_cgB(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArg
     return launch_cgB_v<8>(c, sg, L, a, it);
 }
 
+// Chronopoulos-Gear CG launches (cg_variant 1)
+template <bool FIRST, bool FOLD>
+static void launch_cc1_t(hip_proj_ctx* c, double* pn, const double* po, const PPrev& pv, double* x,
+                         int it) {
+    const unsigned n = (unsigned)(c->px / 2) * (unsigned)(c->ny - 2) *
+                       (unsigned)(c->sgeo.k1 - c->sgeo.k0);
+    const unsigned nb = std::max(1u, std::min((n + 255) / 256, (unsigned)c->grid_cap * 4));
+    hipExtLaunchKernelGGL((k_cc1<FIRST, FOLD>), dim3(nb), dim3(256), 0, c->stream, c->ta, c->tb, 0,
+                          c->sgeo, c->r, c->cw, c->cs, po, pn, pv, x, c->st, it);
+}
+
+static void launch_cc1(hip_proj_ctx* c, double* pn, const double* po, const PPrev& pv, double* x,
+                       int it) {
+    const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
+    if (it == 0) launch_cc1_t<true, false>(c, pn, po, pv, x, it);
+    else if (fold) launch_cc1_t<false, true>(c, pn, po, pv, x, it);
+    else launch_cc1_t<false, false>(c, pn, po, pv, x, it);
+}
+
+template <int TY, bool DIST, bool INIT>
+static void launch_cc2_t(hip_proj_ctx* c, const Lap& L, int it) {
+    hipExtLaunchKernelGGL((k_cc2<TY, DIST, INIT>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
+                          c->stream, c->ta, c->tb, 0, c->sgeo, L, c->r, c->cw, c->st, c->partials,
+                          c->counter, it, c->dsum, mbox(c));
+}
+
+template <int TY>
+static void launch_cc2_ty(hip_proj_ctx* c, const Lap& L, int it, bool init) {
+    if (dist(c)) init ? launch_cc2_t<TY, true, true>(c, L, it) : launch_cc2_t<TY, true, false>(c, L, it);
+    else init ? launch_cc2_t<TY, false, true>(c, L, it) : launch_cc2_t<TY, false, false>(c, L, it);
+}
+
+static void launch_cc2(hip_proj_ctx* c, const Lap& L, int it, bool init) {
+    if (c->sweep_ty == 16) return launch_cc2_ty<16>(c, L, it, init);
+    if (c->sweep_ty == 4) return launch_cc2_ty<4>(c, L, it, init);
+    return launch_cc2_ty<8>(c, L, it, init);
+}
+
 // ---------------------------------------------------------------------------
 // pressure solvers on ctx->pn
 // ---------------------------------------------------------------------------
@@ -188,8 +226,12 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         const int kb = fold ? HIP_KT_CG_SWEEP_BX : HIP_KT_CG_SWEEP_B;
         timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, it); }, it);
         if (D && !mbox(c)) {
-            ST_TRY(reduce_dot(c));
-            hipExtLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->st, c->dsum + 1, it);
+            ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
+                ST_TRY(reduce_dot(c));
+                hipLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->st,
+                                   c->dsum + 1, it);
+                return CFD_SUCCESS;
+            }, it));
         }
         if (!D) timed(c, kb, [&] { launch_cgB(c, c->sgeo, L, ba, it); }, it);
         if (D) {
@@ -203,21 +245,59 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
             HIP_TRY(hipEventRecord(c->ev_b, c->stream));
             HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
             double* rr[1] = {c->r};
-            ST_TRY(c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false));
+            ST_TRY(timed_span(c, c->hstream, HIP_KT_HALO, [&] {
+                return c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false);
+            }, it));
             HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
             if (c->split_b) timed(c, kb, [&] { launch_cgB(c, c->sg_int, L, ba, it); }, it);
             if (!mbox(c)) {
-                ST_TRY(reduce_dot(c));
-                hipExtLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
-                                      c->st, c->dsum + 1, it, fold ? 1 : 0);
+                ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
+                    ST_TRY(reduce_dot(c));
+                    hipLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->st,
+                                       c->dsum + 1, it, fold ? 1 : 0);
+                    return CFD_SUCCESS;
+                }, it));
             }
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
         }
         return CFD_SUCCESS;
     };
+    // Chronopoulos-Gear (cg_variant 1): k_cc1 (pointwise) -> halo of r ->
+    // k_cc2 (w = A r and both dots, ONE reduction / all-reduce)
+    const bool cc = (c->cfg.cg_variant == 1);
+    auto reduce_cc = [&](int it, bool init) -> cfd_status_t {
+        if (!D || mbox(c)) return CFD_SUCCESS;
+        return timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
+            ST_TRY(c->comm->allreduce_sum(c->stream, c->dsum, c->dsum + 2, 2));
+            hipLaunchKernelGGL(k_finish_cc, dim3(1), dim3(64), 0, c->stream, c->st, c->dsum + 2,
+                               it, (it % CG_XFOLD) == CG_XFOLD - 1 ? 1 : 0, init ? 1 : 0);
+            return CFD_SUCCESS;
+        }, it);
+    };
+    auto iterate_cc = [&](int it) -> cfd_status_t {
+        double* pnew = P[it % CG_XFOLD];
+        double* pold = P[(it + CG_XFOLD - 1) % CG_XFOLD];
+        PPrev pv;
+        for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];
+        timed(c, HIP_KT_CC_UPDATE, [&] { launch_cc1(c, pnew, pold, pv, x, it); }, it);
+        if (D)
+            ST_TRY(timed_span(c, c->stream, HIP_KT_HALO,
+                              [&] { return halo(c, {c->r}); }, it));
+        timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false); }, it);
+        return reduce_cc(it, false);
+    };
+    if (cc) {
+        const size_t n = field_elems(c);
+        if (!c->cw) ST_TRY(dalloc(c, &c->cw, n));
+        if (!c->cs) ST_TRY(dalloc(c, &c->cs, n));
+        // w_0 = A r_0 and alpha_0 (the textbook's first (p, Ap) with p_0 = r_0)
+        timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, -1, true); });
+        ST_TRY(reduce_cc(-1, true));
+    }
+    auto step_it = [&](int it) { return cc ? iterate_cc(it) : iterate(it); };
     int it = 0;
     if (max_iter > 0) {
-        ST_TRY(iterate(0));
+        ST_TRY(step_it(0));
         it = 1;
     }
     // Host polls a pinned copy of the device state once per chunk, one chunk
@@ -228,7 +308,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     int slot = 0, prev = -1;
     while (it < max_iter) {
         const int n = std::min(chunk, max_iter - it);
-        for (int q = 0; q < n; ++q, ++it) ST_TRY(iterate(it));
+        for (int q = 0; q < n; ++q, ++it) ST_TRY(step_it(it));
         HIP_TRY(hipMemcpyAsync(&c->h_state[slot], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
                                c->stream));
         HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
@@ -584,6 +664,7 @@ hip_proj_config_t hip_proj_config_default(void) {
     c.sweep_variant_fold = 0;
     c.dirty_faces = 0;
     c.dirty_sync_interval = 0;
+    c.cg_variant = 0;
     return c;
 }
 
@@ -759,7 +840,8 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     if (dalloc(c, &c->src_v_col, nx) != CFD_SUCCESS) return CFD_ERROR;
     HIP_TRY(hipMalloc((void**)&c->st, sizeof(CgState)));
     HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
-    HIP_TRY(hipMalloc((void**)&c->partials, sizeof(double) * n_partials));
+    // x2: the single-reduction CG reduces two values per workgroup
+    HIP_TRY(hipMalloc((void**)&c->partials, 2 * sizeof(double) * n_partials));
     HIP_TRY(hipMalloc((void**)&c->counter, 64));
     HIP_TRY(hipMemsetAsync(c->counter, 0, 64, c->stream));
     HIP_TRY(hipMalloc((void**)&c->red, 8 * sizeof(unsigned long long)));

@@ -99,6 +99,11 @@ typedef struct {
                                      same host arrays go on. Single-device contexts. */
     int dirty_sync_interval;      /* resident mode: full download every N-th step (0 = only
                                      on hip_proj_sync_host / failure) */
+    int cg_variant;               /* 0 = textbook CG, the reference's loop (linear_solver_cg.c:
+                                     367-439; default); 1 = Chronopoulos-Gear CG: both dot
+                                     products of an iteration in ONE reduction (one
+                                     all-reduce per iteration on Z-slabs), same stopping rule
+                                     and stats, iterates equal to rounding only */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
@@ -125,7 +130,12 @@ typedef enum {
     HIP_KT_ENERGY = 7,     /* energy equation (alpha > 0) */
     HIP_KT_RK_STAGE = 8,   /* one fused RK4 stage (RHS + stage update) */
     HIP_KT_CG_SWEEP_BX = 9,/* odd iterations: sweep B + x += alpha p of both iterations */
-    HIP_KT_COUNT = 10
+    HIP_KT_CC_UPDATE = 10, /* cg_variant 1: p, s, r (and the x fold) update */
+    HIP_KT_CC_SPMV = 11,   /* cg_variant 1: w = A r + (r,r), (w,r) */
+    HIP_KT_HALO = 12,      /* Z-slabs: CG halo exchange (span on its stream) */
+    HIP_KT_ALLREDUCE = 13, /* Z-slabs: RCCL all-reduce of a CG dot (+ finish kernel); the
+                              device-mailbox reduction runs inside the sweep instead */
+    HIP_KT_COUNT = 14
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);

@@ -126,6 +126,31 @@ def main():
                 ohist.append((it, st.max_velocity, st.max_pressure))
             check(name, parts, f, ohist, exact=False)
 
+    # single-reduction CG (cg_variant 1): one all-reduce of two values per
+    # iteration (mailbox or ncclAllReduce); against the textbook oracle to
+    # the variant's gate (iterations +-2, fields 1e-6)
+    g, f, p = cases.cavity(33, 33, 33, Re=100.0, dt=5e-4)
+    parts = run_case(comm, "cc-cavity", g, f, p, 3, cavity_bc, cg_variant=1)
+    if RANK == 0:
+        ohist = []
+        for _ in range(3):
+            api.cavity_bc(f, 1.0)
+            s, st, it = oracle.projection_step(f, g, p, A.ORACLE_POISSON_CG)
+            ohist.append(it)
+        hists = [h for _, h in parts]
+        if any(h != hists[0] for h in hists):
+            failures.append(f"cc-cavity: ranks disagree on state {hists}")
+        if any(abs(h[0] - io) > 2 for h, io in zip(hists[0], ohist)):
+            failures.append(f"cc-cavity: iterations {[h[0] for h in hists[0]]} vs {ohist}")
+        for k in ("u", "v", "w"):
+            got = np.full(getattr(f, k).shape, np.nan)
+            for (a, b, d), _ in parts:
+                got[a:b] = d[k]
+            ref = getattr(f, k)
+            err = float(np.max(np.abs(got - ref))) / max(1e-300, float(np.max(np.abs(ref))))
+            if not err <= 1e-6:
+                failures.append(f"cc-cavity: field {k} rel err {err}")
+
     comm.close()
     ok = [not failures]
     dist.broadcast_object_list(ok, src=0)

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-iteration device time of the two CG variants (hip_proj_config_t.cg_variant
+0 = textbook, 1 = single-reduction Chronopoulos-Gear) on one GPU, at 512^3 and
+on one 8-rank slab's worth of planes (512 x 512 x 66: 64 owned planes + the
+two halo planes). Exactly ITERS iterations (tolerance 0), kernel times from the
+context's event timers. One JSON line per (shape, variant).
+
+usage: ITERS=100 python tools/cg_variant_bench.py
+"""
+import json
+import os
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+from cfd_amd import _abi as A  # noqa: E402
+from cfd_amd import api  # noqa: E402
+
+
+def main():
+    iters = int(os.environ.get("ITERS", "100"))
+    shapes = [(512, 512, 512), (512, 512, 66)]
+    rng = np.random.default_rng(1)
+    for nx, ny, nz in shapes:
+        rhs = np.zeros((nz, ny, nx))
+        rhs[1:-1, 1:-1, 1:-1] = rng.standard_normal((nz - 2, ny - 2, nx - 2))
+        h = 1.0 / (nx - 1)
+        for variant in (0, 1):
+            ctx = api.HipProjection(nx, ny, nz, cg_variant=variant)
+            prm = api._native.host().poisson_solver_params_default()
+            prm.max_iterations = iters
+            prm.tolerance = 0.0
+            prm.absolute_tolerance = 0.0
+            x = np.zeros_like(rhs)
+            ctx.poisson_solve(A.HIP_POISSON_CG, x, rhs, h, h, h, prm)  # warm-up
+            ctx.reset_timing()
+            ctx.enable_timing(True)
+            x[...] = 0.0
+            s, st = ctx.poisson_solve(A.HIP_POISSON_CG, x, rhs, h, h, h, prm)
+            ctx.enable_timing(False)
+            kt = ctx.timing()
+            ctx.close()
+            per = {k: round(v[0] / st.iterations, 4) for k, v in kt.items() if v[1]}
+            loop = sum(v for k, v in per.items() if k != "cg_setup")
+            cells = (nx - 2) * (ny - 2) * (nz - 2)
+            print(json.dumps({"run": "cg_variant", "grid": [nx, ny, nz], "cg_variant": variant,
+                              "iterations": st.iterations, "status": s,
+                              "final_residual": st.final_residual,
+                              "kernel_ms_per_iter": per,
+                              "loop_ms_per_iter": round(loop, 4),
+                              "MLUPS_cg_iter": round(cells / (loop * 1e-3) / 1e6, 1)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
