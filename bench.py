@@ -376,27 +376,52 @@ def pmc_profile(cells):
 
 def cpu_baseline(n, args, k_gpu):
     """The oracle (OpenMP port of the reference projection) timed on this host
-    on a bounded sample of the same step, in a child process that holds no HIP
-    runtime and whose OpenMP runtime starts with OMP_PROC_BIND=close
-    OMP_PLACES=cores (oracle/cpu_baseline.py). Threads: every CPU of this
-    process's affinity mask, but no more than an OMP_NUM_THREADS the box sets
-    (the GPU pool gives each 1-GPU box a 16-CPU share and sets it to 16)."""
+    on a bounded sample of the same step, in child processes that hold no HIP
+    runtime (oracle/cpu_baseline.py). Threads: every CPU of this process's
+    affinity mask, but no more than an OMP_NUM_THREADS the box sets (the GPU
+    pool gives each 1-GPU box a 16-CPU share of a 256-CPU host and sets it to
+    16; the mask still shows all 256). Two placements, since the host is
+    shared with other boxes: OMP_PROC_BIND=close OMP_PLACES=cores (threads on
+    the first cores of the mask) and unbound (the OS picks idle CPUs); the
+    faster is the reported value, both are recorded."""
     import subprocess
 
     affinity = len(os.sched_getaffinity(0))
     env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = min(affinity, env_threads) if env_threads > 0 else affinity
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close",
-               OMP_PLACES="cores", CFD_AMD_NO_TORCH="1")
-    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--size", str(n), "--dt", str(args.dt),
-           "--re", str(args.re), "--k-gpu", str(k_gpu), "--cg-iters", str(args.cpu_cg_iters),
-           "--scalar-cg-iters", str(args.cpu_scalar_cg_iters)]
-    r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
-                       timeout=args.cpu_timeout)
-    if r.returncode != 0:
-        return {"error": f"cpu baseline exit {r.returncode}: {r.stderr.strip()[-400:]}"}
-    out = json.loads(r.stdout.strip().splitlines()[-1])
+    runs = {}
+    for name, bind in (("bound", {"OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}),
+                       ("unbound", {"OMP_PROC_BIND": "false"})):
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads), CFD_AMD_NO_TORCH="1", **bind)
+        if name == "unbound":
+            env.pop("OMP_PLACES", None)
+        cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--size", str(n), "--dt",
+               str(args.dt), "--re", str(args.re), "--k-gpu", str(k_gpu), "--cg-iters",
+               str(args.cpu_cg_iters),
+               "--scalar-cg-iters", str(args.cpu_scalar_cg_iters if name == "bound" else 0)]
+        try:
+            r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
+                               timeout=args.cpu_timeout)
+        except subprocess.TimeoutExpired:
+            runs[name] = {"error": f"timeout {args.cpu_timeout} s"}
+            continue
+        if r.returncode != 0:
+            runs[name] = {"error": f"exit {r.returncode}: {r.stderr.strip()[-400:]}"}
+            continue
+        runs[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    ok = {k: v for k, v in runs.items() if "value" in v}
+    if not ok:
+        return {"error": "cpu baseline failed", "runs": runs}
+    best = max(ok, key=lambda k: ok[k]["value"])
+    out = dict(ok[best])
+    out["placement"] = best
+    out["placements"] = {k: {"value": v.get("value"), "cg_iter_ms": v.get("cg_iter_ms"),
+                             "error": v.get("error")} for k, v in runs.items()}
+    if "scalar_1core" not in out and "bound" in ok:
+        out["scalar_1core"] = ok["bound"].get("scalar_1core")
     out["omp_num_threads_env"] = env_threads or None
+    out["cores_note"] = (f"{threads} threads: the box's CPU share (OMP_NUM_THREADS={env_threads}) "
+                         f"of an affinity mask of {affinity} CPUs on a shared host")
     return out
 
 
