@@ -33,8 +33,9 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
-BYTES_SWEEP_B = 24.0    # non-fold iterations: read p, r; write r
-BYTES_SWEEP_BX = 64.0   # every 4th iteration: + read x, p_{it-3..it-1}; write x (4 alpha p folded)
+BYTES_SWEEP_B = 24.0    # read p, r; write r
+BYTES_SWEEP_AX = 56.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2}; write x
+                        # (the 4 pending alpha p folded; p_{it-1} is sweep A's p_old)
 BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
 BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
@@ -182,7 +183,7 @@ def main():
     mlups = n_int * args.steps / elapsed / 1e6
     k_mean = sum(iters) / len(iters)
     # SURVEY.md §8d credit: (176 + 80 k) B/cell per step (textbook CG moves 80 B
-    # per iteration; ours moves 58, so this figure can exceed what HBM carried)
+    # per iteration; ours moves 56, so this figure can exceed what HBM carried)
     credited = (BYTES_STEP_FIXED_SURVEY + BYTES_CG_ITER_SURVEY * k_mean) * n_int
     credited_gbps = credited * args.steps / elapsed / 1e9
 
@@ -198,8 +199,9 @@ def main():
              BYTES_SWEEP_A),
             ("cg_sweep_b", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, false>",
              BYTES_SWEEP_B),
-            ("cg_sweep_bx", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, true>",
-             BYTES_SWEEP_BX))
+            ("cg_sweep_bx",
+             f"k_cgA<{args.sweep_rows}, false, {dflag}, {args.sweep_variant & ~4}, true>",
+             BYTES_SWEEP_AX))
     for key, kname, bpc in sweep_set:
         ms, cnt = kt[key]
         avg = ms / cnt if cnt else None
@@ -207,11 +209,10 @@ def main():
         sweeps[key] = (kname, bpc, avg, cnt, ach, ms)
     if args.cg_variant == 1:  # one iteration = update + SpMV
         cg_iter_ms = (sweeps["cc_update"][2] or 0.0) + (sweeps["cc_spmv"][2] or 0.0)
-    else:  # one CG iteration = sweep A + the mean of the two sweep B forms
-        avg_a = sweeps["cg_sweep_a"][2] or 0.0
-        nb = sweeps["cg_sweep_b"][3] + sweeps["cg_sweep_bx"][3]
-        avg_b = (sweeps["cg_sweep_b"][5] + sweeps["cg_sweep_bx"][5]) / nb if nb else 0.0
-        cg_iter_ms = avg_a + avg_b
+    else:  # one CG iteration = the mean of the two sweep A forms + sweep B
+        na = sweeps["cg_sweep_a"][3] + sweeps["cg_sweep_bx"][3]
+        avg_a = (sweeps["cg_sweep_a"][5] + sweeps["cg_sweep_bx"][5]) / na if na else 0.0
+        cg_iter_ms = avg_a + (sweeps["cg_sweep_b"][2] or 0.0)
     # roofline on the dominant sweep (largest total time)
     dom = max(sweeps, key=lambda k: sweeps[k][5])
     kname, bpc_dom, avg_dom, _, ach_dom, _ = sweeps[dom]

@@ -247,7 +247,8 @@ __device__ __forceinline__ void fin_setup(CgState* st, double tot, double rel_to
 }
 
 // after (p, Ap): alpha or pAp breakdown (linear_solver_cg.c:395-407)
-__device__ __forceinline__ void fin_A(CgState* st, double tot, int it) {
+__device__ __forceinline__ void fin_A(CgState* st, double tot, int it, bool fold = false) {
+    if (fold) st->xdone = it;  // this sweep A folded alpha_j p_j, j < it, into x
     st->pAp = tot;
     if (fabs(tot) < 1e-30) {
         st->done = 1;
@@ -295,8 +296,8 @@ static __global__ void k_finish_setup(CgState* st, const double* tot, double rel
                                int max_iter, int check_interval) {
     if (threadIdx.x == 0) fin_setup(st, tot[0], rel_tol, abs_tol, max_iter, check_interval);
 }
-static __global__ void k_finish_A(CgState* st, const double* tot, int it) {
-    if (threadIdx.x == 0 && !st->done) fin_A(st, tot[0], it);
+static __global__ void k_finish_A(CgState* st, const double* tot, int it, int fold) {
+    if (threadIdx.x == 0 && !st->done) fin_A(st, tot[0], it, fold != 0);
 }
 static __global__ void k_finish_B(CgState* st, const double* tot, int it, int fold) {
     if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it, fold != 0);
@@ -512,19 +513,38 @@ __device__ __forceinline__ double2 fma2p(double2 a, double beta, double2 b) {
 }
 
 // Sweep A (iteration it):  p_it = r + beta p_{it-1} (FIRST: p = r), written
-// to pnew; (p, A p) with A p in registers. x is not touched here: sweep B of
-// every odd iteration folds the last two alpha p terms into x.
-template <int TY, bool FIRST, bool DIST, int FL = 0>
+// to pnew; (p, A p) with A p in registers.
+// FOLD (it % CG_XFOLD == 0, it > 0): x = (((x + a_{it-4} p_{it-4}) +
+// a_{it-3} p_{it-3}) + a_{it-2} p_{it-2}) + a_{it-1} p_{it-1}, the
+// reference's per-iteration updates x += alpha p (linear_solver_cg.c:379-380,
+// axpy :85-96) in their order with the partial sums in registers, so x is
+// bitwise the reference's while it is read and written every fourth
+// iteration only. p_{it-1} = p_old is already streamed by this sweep and
+// p_{it-4} is the ring slot p_it is written to (read before the write, same
+// lane), so the fold costs x, p_{it-3}, p_{it-2} and the x store.
+struct PFold {
+    const double* q3;  // p_{it-3}
+    const double* q2;  // p_{it-2}
+    double* x;
+};
+
+template <int TY, bool FIRST, bool DIST, int FL = 0, bool FOLD = false>
 static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     SGeo g, Lap L, const double* __restrict__ r, const double* __restrict__ po,
     double* __restrict__ pn, CgState* st, double* partials, unsigned* counter, int it,
-    double* dsum, Mbox* mb) {
+    double* dsum, Mbox* mb, PFold fd) {
     constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
     const double beta = FIRST ? 0.0 : st->beta;
+    double fa[CG_XFOLD];  // alpha_{it-4} .. alpha_{it-1}
+#pragma unroll
+    for (int q = 0; q < CG_XFOLD; ++q) fa[q] = FOLD ? st->alpha[(it + q) % CG_XFOLD] : 0.0;
+    const double* __restrict__ fq3 = fd.q3;
+    const double* __restrict__ fq2 = fd.q2;
+    double* __restrict__ fx = fd.x;
     RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
@@ -544,6 +564,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     struct Bundle {
         double2 cr, co, hr, ho;
         double lr, lo, rr, ro;
+        double2 fxo, f4, f3, f2;  // FOLD: x, p_{it-4}, p_{it-3}, p_{it-2} of plane k
     };
     auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
         const double2 zero = make_double2(0.0, 0.0);  // a value, not the captured object
@@ -569,6 +590,11 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
             b.rr = eok_r ? r[ix + 2] : 0.0;
             b.ro = (eok_r && !FIRST) ? po[ix + 2] : 0.0;
         }
+        const bool fl = FOLD && xok && c.act;
+        b.fxo = fl ? ld2v<FL>(fx, ix) : zero;
+        b.f4 = fl ? ld2v<FL>(pn, ix) : zero;
+        b.f3 = fl ? ld2v<FL>(fq3, ix) : zero;
+        b.f2 = fl ? ld2v<FL>(fq2, ix) : zero;
         return b;
     };
     auto form2 = [&](double2 a, double2 b) { return FIRST ? a : fma2p(a, beta, b); };
@@ -576,7 +602,9 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     double acc = 0.0;
     long long idx = c.idx;
     double2 pm = xok ? form2(ld2(r, idx - g.sz), FIRST ? zero : ld2(po, idx - g.sz)) : zero;
-    double2 pc = xok ? form2(ld2(r, idx), FIRST ? zero : ld2(po, idx)) : zero;
+    // raw p_{it-1} of the current plane (the fold's last term)
+    double2 praw = (FOLD && xok) ? ld2(po, idx) : zero;
+    double2 pc = xok ? form2(ld2(r, idx), FIRST ? zero : (FOLD ? praw : ld2(po, idx))) : zero;
     double2 hc = (xok && halo) ? form2(ld2(r, idx + hoff), FIRST ? zero : ld2(po, idx + hoff))
                                : zero;
     // Z-slabs: p is pointwise in r and p_old, so the tiles at the slab ends
@@ -610,6 +638,16 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
         if (c.lane == 63) right = E1 ? form1(cur.lr, cur.lo) : form1(cur.rr, cur.ro);
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
+        if (FOLD && c.act) {
+            double2 xw;
+            xw.x = c.in0 ? (((cur.fxo.x + fa[0] * cur.f4.x) + fa[1] * cur.f3.x) + fa[2] * cur.f2.x) +
+                               fa[3] * praw.x
+                         : cur.fxo.x;
+            xw.y = c.in1 ? (((cur.fxo.y + fa[0] * cur.f4.y) + fa[1] * cur.f3.y) + fa[2] * cur.f2.y) +
+                               fa[3] * praw.y
+                         : cur.fxo.y;
+            st2v<FL>(fx, idx, xw);
+        }
         if (c.act) {
             double2 pw;
             pw.x = c.in0 ? pc.x : 0.0;
@@ -620,6 +658,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
         if (c.in1) acc += pc.y * Ap1;
         pm = pc;
         pc = pp;
+        if (FOLD) praw = cur.co;
         hc = form2(cur.hr, cur.ho);
         if (PF) cur = nxt;
         buf ^= 1;
@@ -642,12 +681,12 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     if (grid_sum_last_n<64 * TY>(bt, partials, counter, shs, &flag, tot) && threadIdx.x == 0) {
         if (DIST && mb) {
             double g;
-            if (mbox_allreduce(mb, tot, &g)) fin_A(st, g, it);
+            if (mbox_allreduce(mb, tot, &g)) fin_A(st, g, it, FOLD);
             else comm_fail(st);
         } else if (DIST) {
             dsum[0] = tot;
         } else {
-            fin_A(st, tot, it);
+            fin_A(st, tot, it, FOLD);
         }
     }
 }

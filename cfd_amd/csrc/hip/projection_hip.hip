@@ -11,66 +11,66 @@
 // iteration, poisson_cg_gpu_solve.cuh:189-203).
 #include "ctx.hpp"
 
-template <int TY, bool FIRST, bool DIST, int FL>
+template <int TY, bool FIRST, bool DIST, int FL, bool FOLD>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
-                         double* pn, int it) {
-    hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST, FL>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
-                          c->stream, c->ta, c->tb, 0, c->sgeo, L, r, po, pn, c->st, c->partials,
-                          c->counter, it, c->dsum, mbox(c));
+                         double* pn, int it, const PFold& fd) {
+    hipExtLaunchKernelGGL((k_cgA<TY, FIRST, DIST, FL, FOLD>), dim3(sweep_grid(c)), dim3(64 * TY),
+                          0, c->stream, c->ta, c->tb, 0, c->sgeo, L, r, po, pn, c->st, c->partials,
+                          c->counter, it, c->dsum, mbox(c), fd);
 }
 
-// Sweep B operands: p = p_it (stencil), r, and for the fold (it % 4 == 3)
-// p_{it-3..it-1} and x.
+// Sweep B operands: p = p_it (stencil) and r.
 struct BArgs {
     const double* p;
     double* r;
-    PPrev pv;
-    double* x;
 };
 
-template <int TY, bool DIST, int FL, bool FOLD>
+template <int TY, bool DIST, int FL>
 static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
     const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
-    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, FOLD>), dim3(nb), dim3(64 * TY), 0, c->stream,
-                          c->ta, c->tb, 0, sg, L, a.p, a.r, a.pv, a.x, c->st, c->partials,
-                          c->counter, it, c->dsum, mbox(c));
+    const PPrev none{};
+    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, false>), dim3(nb), dim3(64 * TY), 0, c->stream,
+                          c->ta, c->tb, 0, sg, L, a.p, a.r, none, (double*)nullptr, c->st,
+                          c->partials, c->counter, it, c->dsum, mbox(c));
 }
 
+// fd.x == nullptr: no fold this iteration
 template <int TY, int FL>
 static void launch_cgA_f(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
-                         const double* po, double* pn, int it) {
+                         const double* po, double* pn, int it, const PFold& fd) {
     const bool d = dist(c);
-    if (first) d ? launch_cgA_t<TY, true, true, FL>(c, L, r, po, pn, it)
-                 : launch_cgA_t<TY, true, false, FL>(c, L, r, po, pn, it);
-    else d ? launch_cgA_t<TY, false, true, FL>(c, L, r, po, pn, it)
-           : launch_cgA_t<TY, false, false, FL>(c, L, r, po, pn, it);
+    if (first) d ? launch_cgA_t<TY, true, true, FL, false>(c, L, r, po, pn, it, fd)
+                 : launch_cgA_t<TY, true, false, FL, false>(c, L, r, po, pn, it, fd);
+    // the fold sweep streams 4 more fields: without the plane prefetch's
+    // second register bundle it fits without spilling
+    else if (fd.x) d ? launch_cgA_t<TY, false, true, (FL & ~SW_PREFETCH), true>(c, L, r, po, pn, it, fd)
+                     : launch_cgA_t<TY, false, false, (FL & ~SW_PREFETCH), true>(c, L, r, po, pn, it, fd);
+    else d ? launch_cgA_t<TY, false, true, FL, false>(c, L, r, po, pn, it, fd)
+           : launch_cgA_t<TY, false, false, FL, false>(c, L, r, po, pn, it, fd);
 }
 
 template <int TY, int FL>
 static void launch_cgB_f(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
-    const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
-    if (dist(c)) fold ? launch_cgB_t<TY, true, FL, true>(c, sg, L, a, it)
-                      : launch_cgB_t<TY, true, FL, false>(c, sg, L, a, it);
-    else fold ? launch_cgB_t<TY, false, FL, true>(c, sg, L, a, it)
-              : launch_cgB_t<TY, false, FL, false>(c, sg, L, a, it);
+    if (dist(c)) launch_cgB_t<TY, true, FL>(c, sg, L, a, it);
+    else launch_cgB_t<TY, false, FL>(c, sg, L, a, it);
 }
 
 template <int TY>
 static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
-                         const double* po, double* pn, int it) {
+                         const double* po, double* pn, int it, const PFold& fd) {
     switch (c->sweep_variant) {
-        case 1: return launch_cgA_f<TY, 1>(c, first, L, r, po, pn, it);
-        case 2: return launch_cgA_f<TY, 2>(c, first, L, r, po, pn, it);
-        case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, it);
-        case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it);
-        case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it);
-        case 15: return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it);
+        case 1: return launch_cgA_f<TY, 1>(c, first, L, r, po, pn, it, fd);
+        case 2: return launch_cgA_f<TY, 2>(c, first, L, r, po, pn, it, fd);
+        case 3: return launch_cgA_f<TY, 3>(c, first, L, r, po, pn, it, fd);
+        case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it, fd);
+        case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it, fd);
+        case 15: return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
-        case 23: if constexpr (TY == 16) return launch_cgA_f<TY, 23>(c, first, L, r, po, pn, it);
+        case 23: if constexpr (TY == 16) return launch_cgA_f<TY, 23>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
-        case 31: if constexpr (TY == 16) return launch_cgA_f<TY, 31>(c, first, L, r, po, pn, it);
+        case 31: if constexpr (TY == 16) return launch_cgA_f<TY, 31>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
-        default: return launch_cgA_f<TY, 0>(c, first, L, r, po, pn, it);
+        default: return launch_cgA_f<TY, 0>(c, first, L, r, po, pn, it, fd);
     }
 }
 
@@ -94,27 +94,13 @@ static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BA
 
 // sweep_ty 8 or 16 (any sweep_variant), 4 (variant 0 only)
 static void launch_cgA(hip_proj_ctx* c, bool first, const Lap& L, const double* r,
-                       const double* po, double* pn, int it) {
-    if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, it);
-    if (c->sweep_ty == 16) return launch_cgA_v<16>(c, first, L, r, po, pn, it);
-    return launch_cgA_v<8>(c, first, L, r, po, pn, it);
-}
-
-// the fold sweep (it % 4 == 3) may use its own memory-hint variant (16-row tiles)
-template <int FL>
-static void launch_cgBX(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
-    if (dist(c)) launch_cgB_t<16, true, FL, true>(c, sg, L, a, it);
-    else launch_cgB_t<16, false, FL, true>(c, sg, L, a, it);
+                       const double* po, double* pn, int it, const PFold& fd) {
+    if (c->sweep_ty == 4) return launch_cgA_f<4, 0>(c, first, L, r, po, pn, it, fd);
+    if (c->sweep_ty == 16) return launch_cgA_v<16>(c, first, L, r, po, pn, it, fd);
+    return launch_cgA_v<8>(c, first, L, r, po, pn, it, fd);
 }
 
 static void launch_cgB(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
-    if (c->sweep_ty == 16 && (it % CG_XFOLD) == CG_XFOLD - 1 && c->sweep_variant_fold) {
-        switch (c->sweep_variant_fold) {
-            case 3: return launch_cgBX<3>(c, sg, L, a, it);
-            case 11: return launch_cgBX<11>(c, sg, L, a, it);
-            default: return launch_cgBX<15>(c, sg, L, a, it);
-        }
-    }
     if (c->sweep_ty == 4) return launch_cgB_f<4, 0>(c, sg, L, a, it);
     if (c->sweep_ty == 16) return launch_cgB_v<16>(c, sg, L, a, it);
     return launch_cgB_v<8>(c, sg, L, a, it);
@@ -219,17 +205,18 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     auto iterate = [&](int it) -> cfd_status_t {
         double* pnew = P[it % CG_XFOLD];
         double* pold = P[(it + CG_XFOLD - 1) % CG_XFOLD];
-        const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
-        PPrev pv;
-        for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];  // p_{it-3+q}
-        const BArgs ba{pnew, c->r, pv, x};
-        const int kb = fold ? HIP_KT_CG_SWEEP_BX : HIP_KT_CG_SWEEP_B;
-        timed(c, HIP_KT_CG_SWEEP_A, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, it); }, it);
+        // x += alpha_j p_j of iterations it-4 .. it-1, folded by sweep A
+        const bool fold = it > 0 && (it % CG_XFOLD) == 0;
+        const PFold fd{P[(it + 1) % CG_XFOLD], P[(it + 2) % CG_XFOLD], fold ? x : nullptr};
+        const BArgs ba{pnew, c->r};
+        const int kb = HIP_KT_CG_SWEEP_B;
+        const int ka = fold ? HIP_KT_CG_SWEEP_BX : HIP_KT_CG_SWEEP_A;
+        timed(c, ka, [&] { launch_cgA(c, it == 0, L, c->r, pold, pnew, it, fd); }, it);
         if (D && !mbox(c)) {
             ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
                 ST_TRY(reduce_dot(c));
                 hipLaunchKernelGGL(k_finish_A, dim3(1), dim3(64), 0, c->stream, c->st,
-                                   c->dsum + 1, it);
+                                   c->dsum + 1, it, fold ? 1 : 0);
                 return CFD_SUCCESS;
             }, it));
         }
@@ -254,7 +241,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                 ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
                     ST_TRY(reduce_dot(c));
                     hipLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->st,
-                                       c->dsum + 1, it, fold ? 1 : 0);
+                                       c->dsum + 1, it, 0);
                     return CFD_SUCCESS;
                 }, it));
             }

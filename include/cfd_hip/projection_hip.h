@@ -81,8 +81,8 @@ typedef struct {
                                      1 = separate colour passes + residual pass with a host
                                      check per iteration (the r01 form); 2 = device loop with
                                      the two colour sweeps */
-    int sweep_variant_fold;       /* memory hints of the x-folding sweep B (every 4th CG
-                                     iteration, 16-row tiles): 0 = sweep_variant; 3, 11, 15 */
+    int sweep_variant_fold;       /* ignored since r02: x is folded by sweep A, with
+                                     sweep_variant's hints (kept for layout stability) */
     int dirty_faces;              /* host-buffer step (hip_proj_step, the plugin's `step`):
                                      0 = upload and download u, v, w, p (T) in full every
                                      step (default); 1 = resident mode: the interior stays in
@@ -129,7 +129,7 @@ typedef enum {
     HIP_KT_RESIDUAL = 6,   /* L-infinity residual for the relaxation methods */
     HIP_KT_ENERGY = 7,     /* energy equation (alpha > 0) */
     HIP_KT_RK_STAGE = 8,   /* one fused RK4 stage (RHS + stage update) */
-    HIP_KT_CG_SWEEP_BX = 9,/* odd iterations: sweep B + x += alpha p of both iterations */
+    HIP_KT_CG_SWEEP_BX = 9,/* every 4th iteration: sweep A + x += alpha p of the previous 4 */
     HIP_KT_CC_UPDATE = 10, /* cg_variant 1: p, s, r (and the x fold) update */
     HIP_KT_CC_SPMV = 11,   /* cg_variant 1: w = A r + (r,r), (w,r) */
     HIP_KT_HALO = 12,      /* Z-slabs: CG halo exchange (span on its stream) */
