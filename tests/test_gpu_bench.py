@@ -49,6 +49,9 @@ def test_bench_one_gpu_contract(hip_lib):
     assert 0 < d["roofline"]["frac"] < 1
     cpu = d["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
+    assert cpu["placement"] in ("bound", "unbound") and set(cpu["placements"]) == {"bound",
+                                                                                 "unbound"}
+    assert d["cg_sweeps"]["cg_sweep_bx"]["kernel"].startswith("k_cgA<")  # the fold sweep
 
 
 @pytest.mark.parametrize("case,world,size", [("cavity", 2, 66), ("tg", 2, 66), ("cavity", 4, 66),
@@ -68,3 +71,13 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
     assert d["n_gpus"] == world and d["value"] > 0 and d["scaling"] == "strong"
     assert d["cpu_baseline"] is None  # CPU baseline at N=1 only
     assert f"z-slab x{world}" in d["config"]["parallelism"]
+    # per-rank device times (sweeps, halo, all-reduce) for reading the 1 -> N curve
+    ranks = d["ranks"]
+    assert [q["rank"] for q in ranks] == list(range(world))
+    for q in ranks:
+        assert q["sweep_ms_per_iter"] > 0 and q["halo_ms_per_iter"] > 0
+        if q["dot_allreduce"] == "ncclAllReduce":
+            assert q["allreduce_ms_per_iter"] > 0
+    # the other CG variant measured beside the timed region
+    cmp = d["cg_variant_compare"]
+    assert cmp["cg_variant"] == 1 and cmp["cg_iters"] > 0 and cmp["ms_per_cg_iter_wall"] > 0
