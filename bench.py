@@ -188,20 +188,8 @@ def main():
     credited_gbps = credited * args.steps / elapsed / 1e9
 
     kt = ctx.timing()
-    dflag = "true" if world > 1 else "false"
     sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s, total ms)
-    if args.cg_variant == 1:
-        sweep_set = (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
-                     ("cc_spmv", f"k_cc2<{args.sweep_rows}, {dflag}, false>", BYTES_CC_SPMV))
-    else:
-        sweep_set = (
-            ("cg_sweep_a", f"k_cgA<{args.sweep_rows}, false, {dflag}, {args.sweep_variant}>",
-             BYTES_SWEEP_A),
-            ("cg_sweep_b", f"k_cgB<{args.sweep_rows}, {dflag}, {args.sweep_variant}, false>",
-             BYTES_SWEEP_B),
-            ("cg_sweep_bx",
-             f"k_cgA<{args.sweep_rows}, false, {dflag}, {args.sweep_variant & ~4}, true>",
-             BYTES_SWEEP_AX))
+    sweep_set = sweep_kernels(args.sweep_rows, world > 1, args.sweep_variant, args.cg_variant)
     for key, kname, bpc in sweep_set:
         ms, cnt = kt[key]
         avg = ms / cnt if cnt else None
@@ -355,6 +343,18 @@ def main():
 # timer -> kernel symbol in the PMC profile (the CG sweeps are named per variant)
 TIMER_KERNEL = {"predictor": "k_pred2<false, 0>", "corrector": "k_corr2<0>",
                 "cg_setup": "k_cg_setup<true, false, true, false>"}
+
+
+def sweep_kernels(rows, dist_, variant, cg_variant):
+    """(timer, kernel symbol as rocprofv3 prints it, algorithmic B/cell) of the
+    CG sweeps a run launches; the symbols key the committed PMC profile."""
+    d = "true" if dist_ else "false"
+    if cg_variant == 1:
+        return (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
+                ("cc_spmv", f"k_cc2<{rows}, {d}, false>", BYTES_CC_SPMV))
+    return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
+            ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, false>", BYTES_SWEEP_B),
+            ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))
 
 
 def pmc_profile(cells):

@@ -1,0 +1,32 @@
+"""The committed PMC profile that bench.py reads `roofline.traffic` and
+`measured_GBps` from (profiles/*traffic*.json): it must be
+a profile of the current HIP sources, and it must hold every kernel symbol the
+default bench run looks up, or the bench line silently reports null."""
+import pytest
+
+import bench
+
+CELLS_512 = float(510 ** 3)
+
+
+def test_profile_is_current_and_complete():
+    prof = bench.pmc_profile(CELLS_512)
+    if prof is None:
+        pytest.xfail("no PMC profile of the current cfd_amd/csrc/hip sources: "
+                     "re-run tools/gpu_profile.sh and commit its traffic.json")
+    have = prof["kernels"]
+    # the default run: 1 rank, 16-row sweeps, variant 15, textbook CG
+    want = [k for _, k, _ in bench.sweep_kernels(16, False, 15, 0)]
+    want += list(bench.TIMER_KERNEL.values())
+    missing = [k for k in want if "hbm_bytes_per_launch" not in have.get(k, {})]
+    assert not missing, missing
+    for k in want:
+        assert have[k]["hbm_bytes_per_launch"] > 0
+
+
+def test_sweep_symbols_track_the_variant():
+    one = dict((t, k) for t, k, _ in bench.sweep_kernels(16, True, 15, 0))
+    assert one["cg_sweep_a"] == "k_cgA<16, false, true, 15, false>"
+    assert one["cg_sweep_bx"] == "k_cgA<16, false, true, 11, true>"
+    cc = dict((t, k) for t, k, _ in bench.sweep_kernels(16, False, 15, 1))
+    assert set(cc) == {"cc_update", "cc_spmv"}
