@@ -34,7 +34,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Algorithmic HBM bytes per interior cell:
 BYTES_SWEEP_A = 24.0    # read r, p_old; write p_new
 BYTES_SWEEP_B = 24.0    # read p, r; write r
-BYTES_SWEEP_AX = 56.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2}; write x
+BYTES_SWEEP_AX = 64.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2}; write x
                         # (the 4 pending alpha p folded; p_{it-1} is sweep A's p_old)
 BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
 BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
@@ -183,7 +183,7 @@ def main():
     mlups = n_int * args.steps / elapsed / 1e6
     k_mean = sum(iters) / len(iters)
     # SURVEY.md §8d credit: (176 + 80 k) B/cell per step (textbook CG moves 80 B
-    # per iteration; ours moves 56, so this figure can exceed what HBM carried)
+    # per iteration; ours moves 58, so this figure can exceed what HBM carried)
     credited = (BYTES_STEP_FIXED_SURVEY + BYTES_CG_ITER_SURVEY * k_mean) * n_int
     credited_gbps = credited * args.steps / elapsed / 1e9
 
