@@ -1955,14 +1955,30 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
         own[s] = orow[s] && lanes_own;
         col[s] = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
     }
+    // Loads are issued unconditionally from clamped (always valid) addresses
+    // and never masked: with the same loads on every control path and no
+    // select right behind them, the compiler's vmcnt counting waits for a
+    // plane only where a step consumes it (a load some path skips, or a
+    // select on the loaded value, forces vmcnt(0) right after the prefetch of
+    // the next plane, i.e. a full memory latency per step). Positions outside
+    // the grid (ld false, k out of range) then hold other cells' values; they
+    // only ever feed boundary cells, which are not updated, and halo lanes,
+    // which are not stored or reduced. Rows without R work (rrow false) load
+    // the adjacent row's rhs, which that row's wave loads too (an L2 hit).
+    long long colx[ROWS], colr[ROWS];
+#pragma unroll
+    for (int s = 0; s < ROWS; ++s) {
+        const int ic = (i0 < g.nx) ? max(i0, 0) : g.nx - 2 - ((g.nx - 2) & 1);
+        const int r = r0w + s;
+        const int jr = j0 + s + (r == 0 ? 1 : (r == 15 ? -1 : 0));
+        colx[s] = (long long)max(min(j0 + s, g.ny - 1), 0) * g.px + ic;
+        colr[s] = (long long)max(min(jr, g.ny - 1), 0) * g.px + ic;
+    }
     auto ldx = [&](int s, int k) -> double2 {
-        return (ld[s] && k >= 0 && k < g.nz) ? ld2(X, (long long)k * g.ps + col[s])
-                                             : make_double2(0.0, 0.0);
+        return ld2(X, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx[s]);
     };
-    auto ldr = [&](int s, int k) -> double2 {  // rows without R work never read rhs
-        return (ld[s] && rrow[s] && k >= 0 && k < g.nz)
-                   ? ld2v<FL>(rhs, (long long)k * g.ps + col[s])
-                   : make_double2(0.0, 0.0);
+    auto ldr = [&](int s, int k) -> double2 {
+        return ld2v<FL>(rhs, (long long)min(max(k, 0), g.nz - 1) * g.ps + colr[s]);
     };
     const double2 zero = make_double2(0.0, 0.0);
     // Step q forms R_{q+1} and updates the second colour of plane q.

@@ -427,10 +427,16 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
         double* xi = X[it & 1];
         double* xo = X[(it + 1) & 1];
         if (single) {
+            static const bool rb1_pf = getenv("CFD_HIP_RB1_PF") != nullptr;  // experiments
             timed(c, HIP_KT_RELAX, [&] {
-                hipExtLaunchKernelGGL((k_rb1<FL, 1, false>), dim3(nb1), dim3(rb1_threads<1>()), 0,
-                                      c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo, c->rhs,
-                                      c->rxst, c->partials, c->counter, it);
+                if (rb1_pf)
+                    hipExtLaunchKernelGGL((k_rb1<FL, 1, true>), dim3(nb1), dim3(rb1_threads<1>()),
+                                          0, c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo,
+                                          c->rhs, c->rxst, c->partials, c->counter, it);
+                else
+                    hipExtLaunchKernelGGL((k_rb1<FL, 1, false>), dim3(nb1), dim3(rb1_threads<1>()),
+                                          0, c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo,
+                                          c->rhs, c->rxst, c->partials, c->counter, it);
             });
         } else if (method == HIP_POISSON_REDBLACK) {
             sweep(RX_RED, xi, xo, it);
