@@ -1905,10 +1905,11 @@ using IntC = std::integral_constant<int, V>;
 //    LDS operand of a step is read right after its barrier (one LDS round
 //    trip per step);
 //  - rhs is not loaded on the two halo rows, which never use it.
-// ROWS > 1 (several rows per wave, fewer waves) and a register plane
-// prefetch (PFQ) are kept as template options: at 512^3 both measured slower
-// (two rows: 190 / 142 VGPRs, one workgroup per CU; prefetch at one row
-// spills), so the product instantiates <FL, 1, false>.
+// ROWS > 1 (several rows per wave, fewer waves) is kept as a template option:
+// at 512^3 it measured slower (two rows: 190 / 142 VGPRs, one workgroup per
+// CU). PFQ = the register-ring prefetch below (r02: 0.90 -> 0.76 ms per
+// iteration at 512^3 on one box, 128 VGPRs, three spills outside the z
+// loop); the product instantiates <FL, 1, true>.
 template <int ROWS>
 constexpr int rb1_threads() { return 64 * 16 / ROWS; }
 template <int ROWS>
@@ -1920,8 +1921,20 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
     const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
     constexpr bool PF = PFQ;
     constexpr int NW = 16 / ROWS;  // waves
-    __shared__ double2 xb[2][16][64];  // X rows by plane parity
-    __shared__ double2 rb[2][16][64];  // R rows by plane parity
+    // X and R rows by plane parity; a row is stored as its 64 .x cells, then
+    // its 64 .y cells, so a pair is one ds_read2/ds_write2_b64 and an x
+    // neighbour (one double of the adjacent lane) a conflict-free ds_read_b64
+    // (with double2 rows those 8-B reads at a 16-B lane stride conflicted)
+    __shared__ double xb[2][16][2][64];
+    __shared__ double rb[2][16][2][64];
+    auto lget = [&](double (&a)[2][16][2][64], int p, int r, int l) __attribute__((always_inline)) {
+        return make_double2(a[p][r][0][l], a[p][r][1][l]);
+    };
+    auto lput = [&](double (&a)[2][16][2][64], int p, int r, int l, double2 v)
+                    __attribute__((always_inline)) {
+        a[p][r][0][l] = v.x;
+        a[p][r][1][l] = v.y;
+    };
     __shared__ double sh[NW];
     __shared__ int flag;
     if (st->done) return;
@@ -1983,40 +1996,55 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
     const double2 zero = make_double2(0.0, 0.0);
     // Step q forms R_{q+1} and updates the second colour of plane q.
     // Per row: X_q, X_{q+1}, X_{q+2} (xm, xc, xp); R_{q-1}, R_q (rmm, rm);
-    // rhs_{q+1} (bq); prefetched X_{q+3} / rhs_{q+2} (nx, nb). Of rhs_q and
-    // R_{q-1} only the component of the cell this step's second-colour
-    // update touches is kept (bmh, rmmh): the pattern alternates per plane,
-    // so the end of step q keeps the component step q + 1 will use.
-    // LDS at the top of step q: X_{q+1} rows in xb[(q+1)&1], R_q rows in rb[q&1].
-    double2 xm[ROWS], xc[ROWS], xp[ROWS], bq[ROWS], rm[ROWS], nx[ROWS], nb[ROWS];
+    // rhs_{q+1} (bq). Of rhs_q and R_{q-1} only the component of the cell
+    // this step's second-colour update touches is kept (bmh, rmmh): the
+    // pattern alternates per plane, so the end of step q keeps the component
+    // step q + 1 will use. LDS at the top of step q: X_{q+1} rows in
+    // xb[(q+1)&1], R_q rows in rb[q&1].
+    // PF (register ring): the X planes sit in a ring of four register slots
+    // and rhs in a ring of two, indexed by the step's phase P = (q - q0) mod 4
+    // at compile time (the z loop is unrolled by four), and step q issues the
+    // loads of X_{q+3} and rhs_{q+2} into the free slots before its barrier:
+    // a full step of latency hiding, and no register copy of a loaded value
+    // (a copy would wait for the load). Without PF the loads are issued at
+    // the end of step q and the three X planes shift through xm, xc, xp.
+    double2 xr[ROWS][4], br[ROWS][2], rm[ROWS];
     double bmh[ROWS], rmmh[ROWS];
 #pragma unroll
     for (int s = 0; s < ROWS; ++s) {
-        xm[s] = ldx(s, kb - 2);
-        xc[s] = ldx(s, kb - 1);
-        xp[s] = ldx(s, kb);
-        bq[s] = ldr(s, kb - 1);
+        xr[s][0] = ldx(s, kb - 2);
+        xr[s][1] = ldx(s, kb - 1);
+        xr[s][2] = ldx(s, kb);
+        xr[s][3] = zero;
+        br[s][0] = ldr(s, kb - 1);
+        br[s][1] = zero;
         rm[s] = zero;
         bmh[s] = rmmh[s] = 0.0;
-        nx[s] = PF ? ldx(s, kb + 1) : zero;
-        nb[s] = PF ? ldr(s, kb) : zero;
-        xb[(kb - 1) & 1][r0w + s][lane] = xc[s];
+        lput(xb, (kb - 1) & 1, r0w + s, lane, xr[s][1]);
     }
     double m = 0.0;
     // E: cell i0 of the pair is the cell both updates of this step touch (the
     // first colour, (i+j+k) odd, of plane q+1 and the second of plane q) in
     // the wave's first row; its second row has the other pattern
-    auto step = [&](auto Ec, int q) __attribute__((always_inline)) {
+    auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
         constexpr bool E = decltype(Ec)::value;
-        double2 fx[ROWS], fb[ROWS];
+        constexpr int P = PF ? decltype(Pc)::value : 0;  // ring phase
+        constexpr int IM = P & 3, IC = (P + 1) & 3, IP = (P + 2) & 3, IN = (P + 3) & 3;
+        constexpr int BQ = P & 1, BN = (P + 1) & 1;
+        if constexpr (PF) {
+#pragma unroll
+            for (int s = 0; s < ROWS; ++s) {
+                xr[s][IN] = ldx(s, q + 3);
+                br[s][BN] = ldr(s, q + 2);
+            }
+        }
+        double2 xm[ROWS], xc[ROWS], xp[ROWS], bq[ROWS];
 #pragma unroll
         for (int s = 0; s < ROWS; ++s) {
-            fx[s] = nx[s];
-            fb[s] = nb[s];
-            if (PF && q + 1 < ke) {
-                nx[s] = ldx(s, q + 4);
-                nb[s] = ldr(s, q + 3);
-            }
+            xm[s] = xr[s][IM];
+            xc[s] = xr[s][IC];
+            xp[s] = xr[s][IP];
+            bq[s] = br[s][BQ];
         }
         __syncthreads();
         const int qa = q + 1;
@@ -2025,14 +2053,13 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
         // the output's LDS operands (R_q rows) are read up front, so one LDS
         // round trip after the barrier serves both halves of the step
         const int wlo = max(r0w - 1, 0), whi = min(r0w + ROWS, 15);
-        const double2 rys = rb[q & 1][wlo][lane];
-        const double2 ryn = rb[q & 1][whi][lane];
+        const double2 rys = lget(rb, q & 1, wlo, lane);
+        const double2 ryn = lget(rb, q & 1, whi, lane);
         double rlr[ROWS];
 #pragma unroll
         for (int s = 0; s < ROWS; ++s) {
             const bool Es = (s & 1) ? !E : E;
-            rlr[s] = Es ? reinterpret_cast<const double*>(&rb[q & 1][r0w + s][lm])[1]
-                        : reinterpret_cast<const double*>(&rb[q & 1][r0w + s][lp])[0];
+            rlr[s] = Es ? rb[q & 1][r0w + s][1][lm] : rb[q & 1][r0w + s][0][lp];
         }
         double2 R[ROWS];
         // ---- R_{q+1} and the residual of X at plane q+1 ----
@@ -2043,10 +2070,11 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
             // demand); one row: let the output's LDS reads rise to the top
             if constexpr (ROWS > 1) __builtin_amdgcn_sched_barrier(0);
             R[s] = xc[s];
-            const double2 ys = (s == 0) ? xb[qa & 1][wlo][lane] : xc[s > 0 ? s - 1 : 0];
-            const double2 yn = (s == ROWS - 1) ? xb[qa & 1][whi][lane] : xc[s < ROWS - 1 ? s + 1 : s];
-            const double left = reinterpret_cast<const double*>(&xb[qa & 1][r0w + s][lm])[1];
-            const double right = reinterpret_cast<const double*>(&xb[qa & 1][r0w + s][lp])[0];
+            const double2 ys = (s == 0) ? lget(xb, qa & 1, wlo, lane) : xc[s > 0 ? s - 1 : 0];
+            const double2 yn =
+                (s == ROWS - 1) ? lget(xb, qa & 1, whi, lane) : xc[s < ROWS - 1 ? s + 1 : s];
+            const double left = xb[qa & 1][r0w + s][1][lm];
+            const double right = xb[qa & 1][r0w + s][0][lp];
             if (!rrow[s] || !qin) continue;
             if (Es) {
                 const double v = sor1(rc, xc[s].x, left, xc[s].y, ys.x, yn.x, xm[s].x, xp[s].x,
@@ -2095,36 +2123,49 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
             rmmh[s] = En ? rm[s].x : rm[s].y;
             rm[s] = R[s];
             bmh[s] = En ? bq[s].x : bq[s].y;
-            xm[s] = xc[s];
-            xc[s] = xp[s];
-            xp[s] = PF ? fx[s] : ldx(s, q + 3);
-            bq[s] = PF ? fb[s] : ldr(s, q + 2);
+            if constexpr (!PF) {
+                xr[s][0] = xc[s];
+                xr[s][1] = xp[s];
+                xr[s][2] = ldx(s, q + 3);
+                br[s][0] = ldr(s, q + 2);
+            }
             // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were
             // last read in step q - 1, before this step's barrier)
-            xb[(q + 2) & 1][r0w + s][lane] = xc[s];
-            rb[(q + 1) & 1][r0w + s][lane] = rm[s];
+            lput(xb, (q + 2) & 1, r0w + s, lane, xp[s]);
+            lput(rb, (q + 1) & 1, r0w + s, lane, rm[s]);
         }
     };
     // E(q) for the wave's first row: ((j0 + q + kofs) & 1) == 0; E(kb - 2) == E(kb)
     const bool E0 = __builtin_amdgcn_readfirstlane(((j0 + kb + g.kofs) & 1) == 0 ? 1 : 0) != 0;
     int q = kb - 2;
-    if (E0) {
-        for (; q + 1 < ke; q += 2) {
-            step(BoolC<true>{}, q);
-            step(BoolC<false>{}, q + 1);
+    auto march = [&](auto E0c) __attribute__((always_inline)) {
+        constexpr bool A = decltype(E0c)::value;
+        using TA = BoolC<A>;
+        using TB = BoolC<!A>;
+        if constexpr (PF) {
+            for (; q + 3 < ke; q += 4) {
+                step(TA{}, IntC<0>{}, q);
+                step(TB{}, IntC<1>{}, q + 1);
+                step(TA{}, IntC<2>{}, q + 2);
+                step(TB{}, IntC<3>{}, q + 3);
+            }
+            if (q < ke) step(TA{}, IntC<0>{}, q);
+            if (q + 1 < ke) step(TB{}, IntC<1>{}, q + 1);
+            if (q + 2 < ke) step(TA{}, IntC<2>{}, q + 2);
+        } else {
+            for (; q + 1 < ke; q += 2) {
+                step(TA{}, IntC<0>{}, q);
+                step(TB{}, IntC<0>{}, q + 1);
+            }
+            if (q < ke) step(TA{}, IntC<0>{}, q);
         }
-        if (q < ke) step(BoolC<true>{}, q);
-    } else {
-        for (; q + 1 < ke; q += 2) {
-            step(BoolC<false>{}, q);
-            step(BoolC<true>{}, q + 1);
-        }
-        if (q < ke) step(BoolC<false>{}, q);
-    }
+    };
+    if (E0) march(BoolC<true>{});
+    else march(BoolC<false>{});
     m = wave_max(m);
     if (lane == 0) sh[w] = m;
     __syncthreads();
-    double* shs = (double*)&xb[0][0][0];
+    double* shs = &xb[0][0][0][0];
     if (threadIdx.x == 0) {
         double a = 0.0;
         for (int v = 0; v < NW; ++v) a = fmax(a, sh[v]);

@@ -427,7 +427,10 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
         double* xi = X[it & 1];
         double* xo = X[(it + 1) & 1];
         if (single) {
-            static const bool rb1_pf = getenv("CFD_HIP_RB1_PF") != nullptr;  // experiments
+            // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the
+            // end-of-step loads (experiments)
+            static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
+                                         atoi(getenv("CFD_HIP_RB1_PF")) == 0);
             timed(c, HIP_KT_RELAX, [&] {
                 if (rb1_pf)
                     hipExtLaunchKernelGGL((k_rb1<FL, 1, true>), dim3(nb1), dim3(rb1_threads<1>()),
