@@ -353,7 +353,7 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
         return (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
                 ("cc_spmv", f"k_cc2<{rows}, {d}, false>", BYTES_CC_SPMV))
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
-            ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, false>", BYTES_SWEEP_B),
+            ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}>", BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))
 
 

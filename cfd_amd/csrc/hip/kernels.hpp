@@ -260,10 +260,8 @@ __device__ __forceinline__ void fin_A(CgState* st, double tot, int it, bool fold
     }
 }
 
-// after (r, r): convergence test, rho breakdown, beta (linear_solver_cg.c:416-445).
-// fold: this sweep B also folded alpha_j p_j, j = it-CG_XFOLD+1 .. it, into x.
-__device__ __forceinline__ void fin_B(CgState* st, double tot, int it, bool fold) {
-    if (fold) st->xdone = it + 1;
+// after (r, r): convergence test, rho breakdown, beta (linear_solver_cg.c:416-445)
+__device__ __forceinline__ void fin_B(CgState* st, double tot, int it) {
     double res = sqrt(tot);
     st->res = res;
     st->iterations = it + 1;
@@ -299,8 +297,8 @@ static __global__ void k_finish_setup(CgState* st, const double* tot, double rel
 static __global__ void k_finish_A(CgState* st, const double* tot, int it, int fold) {
     if (threadIdx.x == 0 && !st->done) fin_A(st, tot[0], it, fold != 0);
 }
-static __global__ void k_finish_B(CgState* st, const double* tot, int it, int fold) {
-    if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it, fold != 0);
+static __global__ void k_finish_B(CgState* st, const double* tot, int it) {
+    if (threadIdx.x == 0 && !st->done) fin_B(st, tot[0], it);
 }
 
 // ---------------------------------------------------------------------------
@@ -692,13 +690,8 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
 }
 
 // Sweep B (iteration it): r -= alpha A p (A p recomputed from p, bitwise equal
-// to sweep A's), rho_new = (r, r), convergence test and beta.
-// FOLD (it % 4 == 3): x = (((x + a_{it-3} p_{it-3}) + a_{it-2} p_{it-2})
-// + a_{it-1} p_{it-1}) + a_it p_it, the reference's per-iteration updates
-// x += alpha p (linear_solver_cg.c:379-380, axpy :85-96) in their order with
-// the partial sums in registers, so x is bitwise the reference's while it is
-// read and written every fourth iteration only (p_{it-3..it-1} are the other
-// buffers of the p ring).
+// to sweep A's), rho_new = (r, r), convergence test and beta. (x is folded by
+// sweep A every CG_XFOLD iterations, k_cgA<FOLD>.)
 struct PRing {
     const double* p[CG_XFOLD];  // p_j at [j % CG_XFOLD]
 };
@@ -706,25 +699,16 @@ struct PPrev {
     const double* q[CG_XFOLD - 1];  // p_{it-3}, p_{it-2}, p_{it-1}
 };
 
-template <int TY, bool DIST, int FL = 0, bool FOLD = false>
+template <int TY, bool DIST, int FL = 0>
 static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
-    SGeo g, Lap L, const double* __restrict__ p, double* __restrict__ r,
-    PPrev pv, double* __restrict__ x, CgState* st, double* partials,
-    unsigned* counter, int it, double* dsum, Mbox* mb) {
+    SGeo g, Lap L, const double* __restrict__ p, double* __restrict__ r, CgState* st,
+    double* partials, unsigned* counter, int it, double* dsum, Mbox* mb) {
     constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     __shared__ double sh[TY];
     __shared__ int flag;
     if (st->done) return;
-    const double acur = st->alpha[it % CG_XFOLD];
-    double aq[CG_XFOLD - 1];
-#pragma unroll
-    for (int q = 0; q < CG_XFOLD - 1; ++q)
-        aq[q] = FOLD ? st->alpha[(it + 1 + q) % CG_XFOLD] : 0.0;  // alpha_{it-3+q}
-    const double* __restrict__ q0 = pv.q[0];
-    const double* __restrict__ q1 = pv.q[1];
-    const double* __restrict__ q2 = pv.q[2];
-    const double malpha = -acur;
+    const double malpha = -st->alpha[it % CG_XFOLD];
     RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
@@ -738,10 +722,10 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     const long long eoff = (c.lane == 0) ? -1 : 2;
     const bool inner = (FL & SW_NT_INNER) && !halo;
     const double2 zero = make_double2(0.0, 0.0);
-    // p of the centre and y-halo row of plane k+1; r, x, p_{it-3..it-1} and
-    // the x-edge p of plane k (SW_EDGE1: both edge cells in el)
+    // p of the centre and y-halo row of plane k+1; r and the x-edge p of
+    // plane k (SW_EDGE1: both edge cells in el)
     struct Bundle {
-        double2 pp, hp, rr, xo, qa, qb, qc;
+        double2 pp, hp, rr;
         double el, er;
     };
     auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
@@ -752,10 +736,6 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         else b.pp = xok ? ld2(p, ip) : zero;
         b.hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
         b.rr = xok ? ld2v<FL>(r, ix) : zero;
-        b.xo = (FOLD && xok) ? ld2v<FL>(x, ix) : zero;
-        b.qa = (FOLD && xok) ? ld2v<FL>(q0, ix) : zero;
-        b.qb = (FOLD && xok) ? ld2v<FL>(q1, ix) : zero;
-        b.qc = (FOLD && xok) ? ld2v<FL>(q2, ix) : zero;
         if (E1) {
             b.el = eok ? p[ix + eoff] : 0.0;
             b.er = 0.0;
@@ -796,16 +776,6 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         rn.x = c.in0 ? cur.rr.x + malpha * Ap0 : cur.rr.x;
         rn.y = c.in1 ? cur.rr.y + malpha * Ap1 : cur.rr.y;
         if (c.act) st2v<FL>(r, idx, rn);
-        if (FOLD && c.act) {
-            double2 xw;
-            xw.x = c.in0 ? (((cur.xo.x + aq[0] * cur.qa.x) + aq[1] * cur.qb.x) +
-                            aq[2] * cur.qc.x) + acur * pc.x
-                         : cur.xo.x;
-            xw.y = c.in1 ? (((cur.xo.y + aq[0] * cur.qa.y) + aq[1] * cur.qb.y) +
-                            aq[2] * cur.qc.y) + acur * pc.y
-                         : cur.xo.y;
-            st2v<FL>(x, idx, xw);
-        }
         if (c.in0) acc += rn.x * rn.x;
         if (c.in1) acc += rn.y * rn.y;
         pm = pc;
@@ -827,12 +797,12 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         threadIdx.x == 0) {
         if (DIST && mb) {
             double g2;
-            if (mbox_allreduce(mb, tot, &g2)) fin_B(st, g2, it, FOLD);
+            if (mbox_allreduce(mb, tot, &g2)) fin_B(st, g2, it);
             else comm_fail(st);
         } else if (DIST) {
             dsum[0] = tot;
         } else {
-            fin_B(st, tot, it, FOLD);
+            fin_B(st, tot, it);
         }
     }
 }

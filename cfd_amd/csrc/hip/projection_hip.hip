@@ -28,10 +28,9 @@ struct BArgs {
 template <int TY, bool DIST, int FL>
 static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
     const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
-    const PPrev none{};
-    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, false>), dim3(nb), dim3(64 * TY), 0, c->stream,
-                          c->ta, c->tb, 0, sg, L, a.p, a.r, none, (double*)nullptr, c->st,
-                          c->partials, c->counter, it, c->dsum, mbox(c));
+    hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(nb), dim3(64 * TY), 0, c->stream, c->ta,
+                          c->tb, 0, sg, L, a.p, a.r, c->st, c->partials, c->counter, it,
+                          c->dsum, mbox(c));
 }
 
 // fd.x == nullptr: no fold this iteration
@@ -241,7 +240,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                 ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
                     ST_TRY(reduce_dot(c));
                     hipLaunchKernelGGL(k_finish_B, dim3(1), dim3(64), 0, c->stream, c->st,
-                                       c->dsum + 1, it, 0);
+                                       c->dsum + 1, it);
                     return CFD_SUCCESS;
                 }, it));
             }
