@@ -22,7 +22,9 @@ from . import _abi as A
 PKG_DIR = Path(__file__).resolve().parent
 LIB_DIR = PKG_DIR / "lib"
 CSRC_DIR = PKG_DIR / "csrc"
-HIP_LIB = LIB_DIR / "libcfd_hip.so"
+# CFD_AMD_HIP_LIB: another build of the library (A/B experiments on one box)
+HIP_LIB = Path(os.environ["CFD_AMD_HIP_LIB"]) if os.environ.get("CFD_AMD_HIP_LIB") else (
+    LIB_DIR / "libcfd_hip.so")
 HOST_LIB = LIB_DIR / "libcfd_host.so"
 
 _lock = threading.Lock()
