@@ -61,6 +61,7 @@ struct hip_proj_ctx {
     SGeo sgeo{};       // row-pair CG sweep tiling
     SGeo sg_edge{}, sg_int{};  // slabs: sweep B split into edge planes + interior
     SGeo rgeo{};               // single-pass RB-SOR tiling (k_rb1)
+    int rb1_tc = 64;           // k_rb1 tile width in x pairs (64, 32, 16)
     SGeo pgeo{};               // predictor / corrector z-march tiling (k_pred2, k_corr2)
     int split_b = 0;
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup

@@ -1840,8 +1840,6 @@ static __global__ void k_rx_finish(RxState* st, const unsigned long long* gred, 
 // same expression as the first pass would, so Y is bitwise the two-pass
 // result.
 // ---------------------------------------------------------------------------
-constexpr int RB1_OX = 124;  // output columns per tile (lanes 1..62)
-constexpr int RB1_OY = 12;   // output rows per tile (waves 2..13)
 
 // One SOR update of a cell (linear_solver_redblack.c:103-112 operation order).
 __device__ __forceinline__ double sor1(const RelaxCoef& rc, double vc, double vl, double vr,
@@ -1865,6 +1863,21 @@ using BoolC = std::integral_constant<bool, V>;
 template <int V>
 using IntC = std::integral_constant<int, V>;
 
+// Tile shapes (r02b). A workgroup is 16 waves; lane l of wave w owns the x
+// pair c = l % TC of tile row r = w + 16 (l / TC), so a tile is TC pairs (2 TC
+// columns) by TR = 1024 / TC rows. Rows w and w + 16 h have the same parity,
+// so the colour pattern of a step stays wave-uniform for every TC. R is
+// recomputed on the tile's one-cell halo: 2 TC - 4 columns and TR - 4 rows are
+// written per tile. TC = 64 (16 rows) loads 1.38x the cells it writes, TC = 32
+// (32 rows) 1.22x, and the narrower tiles also waste less on the last x tile
+// (512: 5 x 124 columns for 510 vs 9 x 60).
+template <int TC>
+constexpr int rb1_rows() { return 1024 / TC; }
+template <int TC>
+constexpr int rb1_ox() { return 2 * TC - 4; }  // output columns per tile
+template <int TC>
+constexpr int rb1_oy() { return 1024 / TC - 4; }  // output rows per tile
+
 // Issue-model details (r02; profiles/r02_rb_variants.jsonl, r02_pmc_rb.jsonl):
 //  - the colour pattern of a step is wave-uniform ((j + q) parity): the z
 //    loop is unrolled by two planes and each step is compiled for its
@@ -1875,32 +1888,25 @@ using IntC = std::integral_constant<int, V>;
 //    LDS operand of a step is read right after its barrier (one LDS round
 //    trip per step);
 //  - rhs is not loaded on the two halo rows, which never use it.
-// ROWS > 1 (several rows per wave, fewer waves) is kept as a template option:
-// at 512^3 it measured slower (two rows: 190 / 142 VGPRs, one workgroup per
-// CU). PFQ = the register-ring prefetch below (r02: 0.90 -> 0.76 ms per
-// iteration at 512^3 on one box, 128 VGPRs, three spills outside the z
-// loop); the product instantiates <FL, 1, true>.
-template <int ROWS>
-constexpr int rb1_threads() { return 64 * 16 / ROWS; }
-template <int ROWS>
-constexpr int rb1_min_waves() { return ROWS == 1 ? 4 : 2; }
-
-template <int FL, int ROWS, bool PFQ>
-static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) void k_rb1(
+// PF = the register-ring prefetch below (r02: 0.90 -> 0.76 ms per iteration at
+// 512^3 on one box, 128 VGPRs); the product instantiates PF = true.
+template <int FL, int TC, bool PF>
+static __global__ __launch_bounds__(1024, 4) void k_rb1(
     SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
     const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
-    constexpr bool PF = PFQ;
-    constexpr int NW = 16 / ROWS;  // waves
-    // X and R rows by plane parity; a row is stored as its 64 .x cells, then
-    // its 64 .y cells, so a pair is one ds_read2/ds_write2_b64 and an x
+    constexpr int NW = 16;  // waves
+    constexpr int TR = rb1_rows<TC>();
+    constexpr int OX = rb1_ox<TC>(), OY = rb1_oy<TC>();
+    // X and R rows by plane parity; a row is stored as its TC .x cells, then
+    // its TC .y cells, so a pair is one ds_read2/ds_write2_b64 and an x
     // neighbour (one double of the adjacent lane) a conflict-free ds_read_b64
     // (with double2 rows those 8-B reads at a 16-B lane stride conflicted)
-    __shared__ double xb[2][16][2][64];
-    __shared__ double rb[2][16][2][64];
-    auto lget = [&](double (&a)[2][16][2][64], int p, int r, int l) __attribute__((always_inline)) {
+    __shared__ double xb[2][TR][2][TC];
+    __shared__ double rb[2][TR][2][TC];
+    auto lget = [&](double (&a)[2][TR][2][TC], int p, int r, int l) __attribute__((always_inline)) {
         return make_double2(a[p][r][0][l], a[p][r][1][l]);
     };
-    auto lput = [&](double (&a)[2][16][2][64], int p, int r, int l, double2 v)
+    auto lput = [&](double (&a)[2][TR][2][TC], int p, int r, int l, double2 v)
                     __attribute__((always_inline)) {
         a[p][r][0][l] = v.x;
         a[p][r][1][l] = v.y;
@@ -1916,28 +1922,27 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
     const int tz = rest / g.tiles_y;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lm = (lane - 1) & 63, lp = (lane + 1) & 63;  // x neighbours' lanes
-    const int i0 = tx * RB1_OX - 2 + 2 * lane;  // even; the pair is (i0, i0 + 1)
-    const int r0w = ROWS * w;                   // tile rows r0w .. r0w + ROWS - 1
-    const int j0 = ty * RB1_OY - 2 + r0w;       // grid row of tile row r0w
+    const int c = lane % TC;                     // pair within the row
+    const int r = w + NW * (lane / TC);          // tile row
+    const int cm = max(c - 1, 0), cp = min(c + 1, TC - 1);  // x neighbours' pairs
+    const int rlo = max(r - 1, 0), rhi = min(r + 1, TR - 1);  // y neighbours' rows
+    const int i0 = tx * OX - 2 + 2 * c;  // even; the pair is (i0, i0 + 1)
+    const int j = ty * OY - 2 + r;       // grid row
     const int kb = g.k0 + tz * g.kc;
     const int ke = min(kb + g.kc, g.k1);
     const bool xin = (i0 >= 0 && i0 < g.nx);
-    const bool lanes_own = (lane >= 1 && lane <= 62);
-    bool ld[ROWS], jin[ROWS], in0[ROWS], in1[ROWS], own[ROWS], orow[ROWS], rrow[ROWS];
-    long long col[ROWS];
-#pragma unroll
-    for (int s = 0; s < ROWS; ++s) {
-        const int j = j0 + s, r = r0w + s;
-        ld[s] = xin && j >= 0 && j < g.ny;
-        jin[s] = (j >= 1 && j <= g.ny - 2);
-        in0[s] = jin[s] && i0 >= 1 && i0 <= g.nx - 2;
-        in1[s] = jin[s] && i0 + 1 <= g.nx - 2;
-        orow[s] = (r >= 2 && r < 2 + RB1_OY);   // wave-uniform
-        rrow[s] = (r >= 1 && r <= 14);          // wave-uniform
-        own[s] = orow[s] && lanes_own;
-        col[s] = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
-    }
+    const bool ld = xin && j >= 0 && j < g.ny;
+    const bool jin = (j >= 1 && j <= g.ny - 2);
+    const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;
+    const bool in1 = jin && i0 + 1 <= g.nx - 2;
+    const bool orow = (r >= 2 && r < 2 + OY);
+    const bool own = orow && c >= 1 && c <= TC - 2;
+    // wave-uniform skips: with TC = 64 a wave is one row, so its halo rows
+    // (no R work: rows 0, 15; no output: rows 0, 1, 14, 15) skip whole
+    // phases; narrower tiles mix rows in a wave and mask per lane instead
+    const bool wr = (TC == 64) ? (r >= 1 && r <= TR - 2) : true;
+    const bool wo = (TC == 64) ? orow : true;
+    const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
     // Loads are issued unconditionally from clamped (always valid) addresses
     // and never masked: with the same loads on every control path and no
     // select right behind them, the compiler's vmcnt counting waits for a
@@ -1946,26 +1951,21 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
     // the next plane, i.e. a full memory latency per step). Positions outside
     // the grid (ld false, k out of range) then hold other cells' values; they
     // only ever feed boundary cells, which are not updated, and halo lanes,
-    // which are not stored or reduced. Rows without R work (rrow false) load
-    // the adjacent row's rhs, which that row's wave loads too (an L2 hit).
-    long long colx[ROWS], colr[ROWS];
-#pragma unroll
-    for (int s = 0; s < ROWS; ++s) {
-        const int ic = (i0 < g.nx) ? max(i0, 0) : g.nx - 2 - ((g.nx - 2) & 1);
-        const int r = r0w + s;
-        const int jr = j0 + s + (r == 0 ? 1 : (r == 15 ? -1 : 0));
-        colx[s] = (long long)max(min(j0 + s, g.ny - 1), 0) * g.px + ic;
-        colr[s] = (long long)max(min(jr, g.ny - 1), 0) * g.px + ic;
-    }
-    auto ldx = [&](int s, int k) -> double2 {
-        return ld2(X, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx[s]);
+    // which are not stored or reduced. The halo rows 0 and TR - 1 (no R work)
+    // load the adjacent row's rhs, which that row's lanes load too (an L2 hit).
+    const int ic = (i0 < g.nx) ? max(i0, 0) : g.nx - 2 - ((g.nx - 2) & 1);
+    const int jr = j + (r == 0 ? 1 : (r == TR - 1 ? -1 : 0));
+    const long long colx = (long long)max(min(j, g.ny - 1), 0) * g.px + ic;
+    const long long colr = (long long)max(min(jr, g.ny - 1), 0) * g.px + ic;
+    auto ldx = [&](int k) -> double2 {
+        return ld2(X, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx);
     };
-    auto ldr = [&](int s, int k) -> double2 {
-        return ld2v<FL>(rhs, (long long)min(max(k, 0), g.nz - 1) * g.ps + colr[s]);
+    auto ldr = [&](int k) -> double2 {
+        return ld2v<FL>(rhs, (long long)min(max(k, 0), g.nz - 1) * g.ps + colr);
     };
     const double2 zero = make_double2(0.0, 0.0);
     // Step q forms R_{q+1} and updates the second colour of plane q.
-    // Per row: X_q, X_{q+1}, X_{q+2} (xm, xc, xp); R_{q-1}, R_q (rmm, rm);
+    // Per lane: X_q, X_{q+1}, X_{q+2} (xm, xc, xp); R_{q-1}, R_q (rmm, rm);
     // rhs_{q+1} (bq). Of rhs_q and R_{q-1} only the component of the cell
     // this step's second-colour update touches is kept (bmh, rmmh): the
     // pattern alternates per plane, so the end of step q keeps the component
@@ -1978,135 +1978,90 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
     // a full step of latency hiding, and no register copy of a loaded value
     // (a copy would wait for the load). Without PF the loads are issued at
     // the end of step q and the three X planes shift through xm, xc, xp.
-    double2 xr[ROWS][4], br[ROWS][2], rm[ROWS];
-    double bmh[ROWS], rmmh[ROWS];
-#pragma unroll
-    for (int s = 0; s < ROWS; ++s) {
-        xr[s][0] = ldx(s, kb - 2);
-        xr[s][1] = ldx(s, kb - 1);
-        xr[s][2] = ldx(s, kb);
-        xr[s][3] = zero;
-        br[s][0] = ldr(s, kb - 1);
-        br[s][1] = zero;
-        rm[s] = zero;
-        bmh[s] = rmmh[s] = 0.0;
-        lput(xb, (kb - 1) & 1, r0w + s, lane, xr[s][1]);
-    }
+    double2 xr[4], br[2], rm;
+    double bmh, rmmh;
+    xr[0] = ldx(kb - 2);
+    xr[1] = ldx(kb - 1);
+    xr[2] = ldx(kb);
+    xr[3] = zero;
+    br[0] = ldr(kb - 1);
+    br[1] = zero;
+    rm = zero;
+    bmh = rmmh = 0.0;
+    lput(xb, (kb - 1) & 1, r, c, xr[1]);
     double m = 0.0;
     // E: cell i0 of the pair is the cell both updates of this step touch (the
-    // first colour, (i+j+k) odd, of plane q+1 and the second of plane q) in
-    // the wave's first row; its second row has the other pattern
+    // first colour, (i+j+k) odd, of plane q+1 and the second of plane q)
     auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
         constexpr bool E = decltype(Ec)::value;
         constexpr int P = PF ? decltype(Pc)::value : 0;  // ring phase
         constexpr int IM = P & 3, IC = (P + 1) & 3, IP = (P + 2) & 3, IN = (P + 3) & 3;
         constexpr int BQ = P & 1, BN = (P + 1) & 1;
         if constexpr (PF) {
-#pragma unroll
-            for (int s = 0; s < ROWS; ++s) {
-                xr[s][IN] = ldx(s, q + 3);
-                br[s][BN] = ldr(s, q + 2);
-            }
+            xr[IN] = ldx(q + 3);
+            br[BN] = ldr(q + 2);
         }
-        double2 xm[ROWS], xc[ROWS], xp[ROWS], bq[ROWS];
-#pragma unroll
-        for (int s = 0; s < ROWS; ++s) {
-            xm[s] = xr[s][IM];
-            xc[s] = xr[s][IC];
-            xp[s] = xr[s][IP];
-            bq[s] = br[s][BQ];
-        }
+        const double2 xm = xr[IM], xc = xr[IC], xp = xr[IP], bq = br[BQ];
         __syncthreads();
         const int qa = q + 1;
         const bool qin = (qa >= g.k0 && qa < g.k1);
         const bool rin = qin && qa >= kb && qa < ke;
         // the output's LDS operands (R_q rows) are read up front, so one LDS
         // round trip after the barrier serves both halves of the step
-        const int wlo = max(r0w - 1, 0), whi = min(r0w + ROWS, 15);
-        const double2 rys = lget(rb, q & 1, wlo, lane);
-        const double2 ryn = lget(rb, q & 1, whi, lane);
-        double rlr[ROWS];
-#pragma unroll
-        for (int s = 0; s < ROWS; ++s) {
-            const bool Es = (s & 1) ? !E : E;
-            rlr[s] = Es ? rb[q & 1][r0w + s][1][lm] : rb[q & 1][r0w + s][0][lp];
-        }
-        double2 R[ROWS];
+        const double2 rys = lget(rb, q & 1, rlo, c);
+        const double2 ryn = lget(rb, q & 1, rhi, c);
+        const double rlr = E ? rb[q & 1][r][1][cm] : rb[q & 1][r][0][cp];
         // ---- R_{q+1} and the residual of X at plane q+1 ----
-#pragma unroll
-        for (int s = 0; s < ROWS; ++s) {
-            const bool Es = (s & 1) ? !E : E;
-            // two rows: one at a time (interleaving them raises the register
-            // demand); one row: let the output's LDS reads rise to the top
-            if constexpr (ROWS > 1) __builtin_amdgcn_sched_barrier(0);
-            R[s] = xc[s];
-            const double2 ys = (s == 0) ? lget(xb, qa & 1, wlo, lane) : xc[s > 0 ? s - 1 : 0];
-            const double2 yn =
-                (s == ROWS - 1) ? lget(xb, qa & 1, whi, lane) : xc[s < ROWS - 1 ? s + 1 : s];
-            const double left = xb[qa & 1][r0w + s][1][lm];
-            const double right = xb[qa & 1][r0w + s][0][lp];
-            if (!rrow[s] || !qin) continue;
-            if (Es) {
-                const double v = sor1(rc, xc[s].x, left, xc[s].y, ys.x, yn.x, xm[s].x, xp[s].x,
-                                      bq[s].x);
-                if (in0[s]) R[s].x = v;
+        double2 R = xc;
+        const double2 ys = lget(xb, qa & 1, rlo, c);
+        const double2 yn = lget(xb, qa & 1, rhi, c);
+        const double left = xb[qa & 1][r][1][cm];
+        const double right = xb[qa & 1][r][0][cp];
+        if (wr && qin) {
+            if (E) {
+                const double v = sor1(rc, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
+                if (in0) R.x = v;
             } else {
-                const double v = sor1(rc, xc[s].y, xc[s].x, right, ys.y, yn.y, xm[s].y, xp[s].y,
-                                      bq[s].y);
-                if (in1[s]) R[s].y = v;
+                const double v = sor1(rc, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
+                if (in1) R.y = v;
             }
-            if (orow[s] && rin) {
-                const double a0 = res1(rc, xc[s].x, left, xc[s].y, ys.x, yn.x, xm[s].x, xp[s].x,
-                                       bq[s].x);
-                const double a1 = res1(rc, xc[s].y, xc[s].x, right, ys.y, yn.y, xm[s].y,
-                                       xp[s].y, bq[s].y);
-                if (own[s] && in0[s] && a0 > m) m = a0;
-                if (own[s] && in1[s] && a1 > m) m = a1;
+            if (wo && rin) {
+                const double a0 = res1(rc, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
+                const double a1 = res1(rc, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
+                if (own && in0 && a0 > m) m = a0;
+                if (own && in1 && a1 > m) m = a1;
             }
         }
         // ---- second colour of plane q from R_{q-1}, R_q, R_{q+1} ----
-        if (q >= kb) {
-#pragma unroll
-            for (int s = 0; s < ROWS; ++s) {
-                const bool Es = (s & 1) ? !E : E;
-                if constexpr (ROWS > 1) __builtin_amdgcn_sched_barrier(0);
-                if (!orow[s]) continue;
-                const double2 ys = (s == 0) ? rys : rm[s > 0 ? s - 1 : 0];
-                const double2 yn = (s == ROWS - 1) ? ryn : rm[s < ROWS - 1 ? s + 1 : s];
-                double2 out = rm[s];
-                if (Es) {
-                    const double v = sor1(rc, rm[s].x, rlr[s], rm[s].y, ys.x, yn.x, rmmh[s],
-                                          R[s].x, bmh[s]);
-                    if (own[s] && in0[s]) out.x = v;
-                } else {
-                    const double v = sor1(rc, rm[s].y, rm[s].x, rlr[s], ys.y, yn.y, rmmh[s],
-                                          R[s].y, bmh[s]);
-                    if (own[s] && in1[s]) out.y = v;
-                }
-                if (own[s] && ld[s] && jin[s]) st2v<FL>(Y, (long long)q * g.ps + col[s], out);
+        if (q >= kb && wo) {
+            double2 out = rm;
+            if (E) {
+                const double v = sor1(rc, rm.x, rlr, rm.y, rys.x, ryn.x, rmmh, R.x, bmh);
+                if (own && in0) out.x = v;
+            } else {
+                const double v = sor1(rc, rm.y, rm.x, rlr, rys.y, ryn.y, rmmh, R.y, bmh);
+                if (own && in1) out.y = v;
             }
+            if (own && ld && jin) st2v<FL>(Y, (long long)q * g.ps + col, out);
         }
-#pragma unroll
-        for (int s = 0; s < ROWS; ++s) {
-            // step q + 1 updates the .x cell of this row iff this step did not
-            const bool En = (s & 1) ? E : !E;
-            rmmh[s] = En ? rm[s].x : rm[s].y;
-            rm[s] = R[s];
-            bmh[s] = En ? bq[s].x : bq[s].y;
-            if constexpr (!PF) {
-                xr[s][0] = xc[s];
-                xr[s][1] = xp[s];
-                xr[s][2] = ldx(s, q + 3);
-                br[s][0] = ldr(s, q + 2);
-            }
-            // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were
-            // last read in step q - 1, before this step's barrier)
-            lput(xb, (q + 2) & 1, r0w + s, lane, xp[s]);
-            lput(rb, (q + 1) & 1, r0w + s, lane, rm[s]);
+        // step q + 1 updates the .x cell iff this step did not
+        rmmh = E ? rm.y : rm.x;
+        rm = R;
+        bmh = E ? bq.y : bq.x;
+        if constexpr (!PF) {
+            xr[0] = xc;
+            xr[1] = xp;
+            xr[2] = ldx(q + 3);
+            br[0] = ldr(q + 2);
         }
+        // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were last
+        // read in step q - 1, before this step's barrier)
+        lput(xb, (q + 2) & 1, r, c, xp);
+        lput(rb, (q + 1) & 1, r, c, rm);
     };
-    // E(q) for the wave's first row: ((j0 + q + kofs) & 1) == 0; E(kb - 2) == E(kb)
-    const bool E0 = __builtin_amdgcn_readfirstlane(((j0 + kb + g.kofs) & 1) == 0 ? 1 : 0) != 0;
+    // E(q) for the lane's row: ((j + q + kofs) & 1) == 0; E(kb - 2) == E(kb);
+    // rows r and r + 16 h share the parity, so E is wave-uniform
+    const bool E0 = __builtin_amdgcn_readfirstlane(((j + kb + g.kofs) & 1) == 0 ? 1 : 0) != 0;
     int q = kb - 2;
     auto march = [&](auto E0c) __attribute__((always_inline)) {
         constexpr bool A = decltype(E0c)::value;
@@ -2148,8 +2103,7 @@ static __global__ __launch_bounds__(rb1_threads<ROWS>(), rb1_min_waves<ROWS>()) 
     __syncthreads();
     if (flag == 0) return;
     double a = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += rb1_threads<ROWS>())
-        a = fmax(a, load_sc1(&partials[b]));
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 1024) a = fmax(a, load_sc1(&partials[b]));
     a = wave_max(a);
     if (lane == 0) shs[w] = a;
     __syncthreads();

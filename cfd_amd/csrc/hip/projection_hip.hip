@@ -430,16 +430,17 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             // end-of-step loads (experiments)
             static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
                                          atoi(getenv("CFD_HIP_RB1_PF")) == 0);
+#define RB1_LAUNCH(TCV, PFV)                                                                   \
+    hipExtLaunchKernelGGL((k_rb1<FL, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
+                          c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
+                          c->counter, it)
             timed(c, HIP_KT_RELAX, [&] {
-                if (rb1_pf)
-                    hipExtLaunchKernelGGL((k_rb1<FL, 1, true>), dim3(nb1), dim3(rb1_threads<1>()),
-                                          0, c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo,
-                                          c->rhs, c->rxst, c->partials, c->counter, it);
-                else
-                    hipExtLaunchKernelGGL((k_rb1<FL, 1, false>), dim3(nb1), dim3(rb1_threads<1>()),
-                                          0, c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo,
-                                          c->rhs, c->rxst, c->partials, c->counter, it);
+                if (!rb1_pf) RB1_LAUNCH(64, false);
+                else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
+                else if (c->rb1_tc == 16) RB1_LAUNCH(16, true);
+                else RB1_LAUNCH(64, true);
             });
+#undef RB1_LAUNCH
         } else if (method == HIP_POISSON_REDBLACK) {
             sweep(RX_RED, xi, xo, it);
             ST_TRY(finish(it));
@@ -779,8 +780,21 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     {
         SGeo& rg = c->rgeo;
         rg = sg;
-        rg.tiles_x = (int)((nx + RB1_OX - 1) / RB1_OX);
-        rg.tiles_y = (int)((ny + RB1_OY - 1) / RB1_OY);
+        // tile width: TC = 64 (128 x 16 cells loaded, 124 x 12 written). The
+        // narrower tiles (32: 64 x 32, 16: 32 x 64) need ~20 % fewer
+        // workgroups at 512^3 and 1024^2 x 512 but mask their halo rows per
+        // lane instead of skipping whole waves, and measured slower (0.846 /
+        // 1.022 vs 0.734 ms at 512^3, profiles/r02_rb_tile_width.jsonl);
+        // CFD_HIP_RB1_TC = 32 / 16 selects them (experiments)
+        int tc = 64;
+        if (const char* e = getenv("CFD_HIP_RB1_TC")) {
+            const int v = atoi(e);
+            if (v == 64 || v == 32 || v == 16) tc = v;
+        }
+        c->rb1_tc = tc;
+        const int ox = 2 * tc - 4, oy = 1024 / tc - 4;
+        rg.tiles_x = (int)((nx - 1 + ox - 1) / ox);
+        rg.tiles_y = (int)((ny - 1 + oy - 1) / oy);
         rg.kc = 64;
         if (const char* e = getenv("CFD_HIP_RB1_KC")) rg.kc = std::max(1, atoi(e));  // experiments
         while (rg.kc > 16 &&

@@ -1,6 +1,6 @@
 """The one-pass Red-Black SOR kernel (k_rb1) against the oracle on shapes
 that exercise its tiling -- partial x and y tiles, z chunks, odd extents,
-early stops -- bit for bit: iterate, iteration count, status, initial and
+early stops, the three tile widths -- bit for bit: iterate, iteration count, status, initial and
 final L-inf residual (linear_solver_redblack.c:80-147,
 linear_solver.c:397-485)."""
 import numpy as np
@@ -20,8 +20,13 @@ pytestmark = pytest.mark.gpu
     ((131, 27, 70), dict(max_iterations=12)),
     ((126, 14, 5), dict(max_iterations=30, check_interval=2)),
     ((255, 50, 140), dict(max_iterations=6)),
+    ((63, 70, 12), dict(max_iterations=9)),
 ])
-def test_rb_one_pass_bitwise(hip_lib, shape, kw):
+@pytest.mark.parametrize("tc", ["64", "32", "16"])
+def test_rb_one_pass_bitwise(hip_lib, shape, kw, tc, monkeypatch):
+    """Every tile width (TC x pairs by 1024 / TC rows), forced through
+    CFD_HIP_RB1_TC, on every shape."""
+    monkeypatch.setenv("CFD_HIP_RB1_TC", tc)
     nx, ny, nz = shape
     rng = np.random.default_rng(nx * 7 + nz)
     rhs = rng.standard_normal((nz, ny, nx))
