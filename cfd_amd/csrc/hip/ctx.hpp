@@ -116,7 +116,7 @@ struct hip_proj_ctx {
     RxState* rxst = nullptr;             // fused relaxation loop state
     double* partials = nullptr;
     unsigned* counter = nullptr;
-    unsigned long long* red = nullptr;   // [0] max vel, [1] max |p|, [2] nonfinite, [3] max T, [4] residual
+    unsigned long long* red = nullptr;   // [0] max |u|^2, [1] max |p|, [2] nonfinite, [3] max T, [4] residual
     CgState* h_state = nullptr;          // pinned, 2 slots + final
     unsigned long long* h_red = nullptr; // pinned, 8
     hipEvent_t ev_poll[2] = {nullptr, nullptr};

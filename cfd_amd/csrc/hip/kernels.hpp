@@ -1436,8 +1436,8 @@ static __global__ __launch_bounds__(256) void k_vel_stats(Geo g, const double* _
         const long long idx = cidx(g, i, j, k);
         const double u = U[idx], v = V[idx], w = W[idx], p = P[idx];
         if (!isfinite(u) || !isfinite(v) || !isfinite(w) || !isfinite(p)) shbad = 1;
-        const double vel = sqrt((u * u) + (v * v) + (w * w));
-        if (vel > mv) mv = vel;
+        const double vel2 = (u * u) + (v * v) + (w * w);  // sqrt on the host (cell_stats)
+        if (vel2 > mv) mv = vel2;
         const double ap = fabs(p);
         if (ap > mp) mp = ap;
     }
@@ -1482,6 +1482,27 @@ __device__ __forceinline__ double divc(double a, double d, double r) {
     const double aq = fabs(q);
     if (!(aq >= 0x1p-900 && aq <= 0x1p+900)) return a / d;  // residual stays normal
     return fma(fma(-q, d, a), r, q);
+}
+
+// Division functors for the stencil helpers. DivC: divc, its range test a
+// branch per division. DivFastZ (below, with divz) defers the test: the fast
+// quotient's range check goes into a lane flag (compare masks, no branch) and
+// the caller recomputes the lanes whose flag dropped with DivExact behind ONE
+// wave-uniform branch; where the flag held the value is divz's, so results
+// are bitwise either way. That form helps the predictor (fewer, longer basic
+// blocks) but spilled in k_rb1 and made it slower (0.845 vs 0.751 ms at
+// 512^3, profiles/r02_deferred_div.jsonl), which keeps DivC.
+struct DivC {  // divc, its range test branching per division
+    __device__ __forceinline__ double operator()(double a, double d, double r) const {
+        return divc(a, d, r);
+    }
+};
+struct DivExact {  // the reference's division (the recompute path)
+    __device__ __forceinline__ double operator()(double a, double d, double) const { return a / d; }
+};
+// true when some lane of the wave dropped its flag (wave-uniform)
+__device__ __forceinline__ bool wave_any_bad(bool ok) {
+    return __builtin_amdgcn_ballot_w64(!ok) != 0;
 }
 
 static __global__ __launch_bounds__(NT) void k_rb_pass(Geo g, RelaxCoef rc, double* __restrict__ x,
@@ -1842,19 +1863,21 @@ static __global__ void k_rx_finish(RxState* st, const unsigned long long* gred, 
 // ---------------------------------------------------------------------------
 
 // One SOR update of a cell (linear_solver_redblack.c:103-112 operation order).
-__device__ __forceinline__ double sor1(const RelaxCoef& rc, double vc, double vl, double vr,
+template <class Dv>
+__device__ __forceinline__ double sor1(const RelaxCoef& rc, Dv dv, double vc, double vl, double vr,
                                        double vs, double vn, double vm, double vp, double vb) {
-    const double pn = -(vb - divc(vr + vl, rc.dx2, rc.rdx2) - divc(vn + vs, rc.dy2, rc.rdy2) -
+    const double pn = -(vb - dv(vr + vl, rc.dx2, rc.rdx2) - dv(vn + vs, rc.dy2, rc.rdy2) -
                         (vp + vm) * rc.inv_dz2) *
                       rc.inv_factor;
     return vc + rc.omega * (pn - vc);
 }
 
 // |lap(x) - rhs| of one cell (linear_solver.c:304-346, the division form).
-__device__ __forceinline__ double res1(const RelaxCoef& rc, double c, double xl, double xr,
+template <class Dv>
+__device__ __forceinline__ double res1(const RelaxCoef& rc, Dv dv, double c, double xl, double xr,
                                        double ys, double yn, double zm, double zp, double b) {
-    const double l = divc(xr - 2.0 * c + xl, rc.dx2, rc.rdx2) +
-                     divc(yn - 2.0 * c + ys, rc.dy2, rc.rdy2) + (zp + zm - 2.0 * c) * rc.inv_dz2;
+    const double l = dv(xr - 2.0 * c + xl, rc.dx2, rc.rdx2) +
+                     dv(yn - 2.0 * c + ys, rc.dy2, rc.rdy2) + (zp + zm - 2.0 * c) * rc.inv_dz2;
     return fabs(l - b);
 }
 
@@ -2011,7 +2034,6 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
         const double2 rys = lget(rb, q & 1, rlo, c);
         const double2 ryn = lget(rb, q & 1, rhi, c);
         const double rlr = E ? rb[q & 1][r][1][cm] : rb[q & 1][r][0][cp];
-        // ---- R_{q+1} and the residual of X at plane q+1 ----
         double2 R = xc;
         const double2 ys = lget(xb, qa & 1, rlo, c);
         const double2 yn = lget(xb, qa & 1, rhi, c);
@@ -2019,15 +2041,15 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
         const double right = xb[qa & 1][r][0][cp];
         if (wr && qin) {
             if (E) {
-                const double v = sor1(rc, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
+                const double v = sor1(rc, DivC{}, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
                 if (in0) R.x = v;
             } else {
-                const double v = sor1(rc, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
+                const double v = sor1(rc, DivC{}, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
                 if (in1) R.y = v;
             }
             if (wo && rin) {
-                const double a0 = res1(rc, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
-                const double a1 = res1(rc, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
+                const double a0 = res1(rc, DivC{}, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
+                const double a1 = res1(rc, DivC{}, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
                 if (own && in0 && a0 > m) m = a0;
                 if (own && in1 && a1 > m) m = a1;
             }
@@ -2036,10 +2058,10 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
         if (q >= kb && wo) {
             double2 out = rm;
             if (E) {
-                const double v = sor1(rc, rm.x, rlr, rm.y, rys.x, ryn.x, rmmh, R.x, bmh);
+                const double v = sor1(rc, DivC{}, rm.x, rlr, rm.y, rys.x, ryn.x, rmmh, R.x, bmh);
                 if (own && in0) out.x = v;
             } else {
-                const double v = sor1(rc, rm.y, rm.x, rlr, rys.y, ryn.y, rmmh, R.y, bmh);
+                const double v = sor1(rc, DivC{}, rm.y, rm.x, rlr, rys.y, ryn.y, rmmh, R.y, bmh);
                 if (own && in1) out.y = v;
             }
             if (own && ld && jin) st2v<FL>(Y, (long long)q * g.ps + col, out);
@@ -2137,7 +2159,10 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
 // nx - 1) are copies; the rest of the boundary shell (rows j = 0, ny - 1, the
 // z faces) is done by k_shell_copy / k_shell_stats.
 // ===========================================================================
-constexpr int PR_TY = 4;  // rows (waves) per workgroup
+#ifndef CFD_PR_TY
+#define CFD_PR_TY 4
+#endif
+constexpr int PR_TY = CFD_PR_TY;  // rows (waves) per workgroup
 
 // a / d correctly rounded, like divc, for operands that are often exactly
 // zero (derivatives of a field at rest): e = q d - a and q - e r give the
@@ -2148,6 +2173,16 @@ __device__ __forceinline__ double divz(double a, double d, double r) {
     if (!(aq <= 0x1p+900 && (aq >= 0x1p-900 || aq == 0.0))) return a / d;
     return fma(-fma(q, d, -a), r, q);
 }
+// divz with the range test deferred into a lane flag (see DivC)
+struct DivFastZ {
+    bool& ok;
+    __device__ __forceinline__ double operator()(double a, double d, double r) const {
+        const double q = a * r;
+        const double aq = fabs(q);
+        ok &= (aq <= 0x1p+900) & ((aq >= 0x1p-900) | (aq == 0.0));
+        return fma(-fma(q, d, -a), r, q);
+    }
+};
 
 struct ZTile {
     int i0, j, kb, ke, lane;
@@ -2197,15 +2232,16 @@ struct PredCoef2 {
 
 // solver_projection.c:121-182 for one cell: c = centre (u, v, w), f = the
 // field the output belongs to (0, 1, 2) with its 6 neighbours
-__device__ __forceinline__ double pred_cell(const PredCoef2& pc, double u, double v, double w,
-                                            double fc, double xm, double xp, double ym,
+template <class Dv>
+__device__ __forceinline__ double pred_cell(const PredCoef2& pc, Dv dv, double u, double v,
+                                            double w, double fc, double xm, double xp, double ym,
                                             double yp, double zm, double zp, double src) {
-    const double d_dx = divz(xp - xm, pc.two_dx, pc.r_two_dx);
-    const double d_dy = divz(yp - ym, pc.two_dy, pc.r_two_dy);
+    const double d_dx = dv(xp - xm, pc.two_dx, pc.r_two_dx);
+    const double d_dy = dv(yp - ym, pc.two_dy, pc.r_two_dy);
     const double d_dz = (zp - zm) * pc.inv_2dz;
     const double conv = u * d_dx + v * d_dy + w * d_dz;
-    const double d2x = divz(xp - 2.0 * fc + xm, pc.dx_sq, pc.r_dx_sq);
-    const double d2y = divz(yp - 2.0 * fc + ym, pc.dy_sq, pc.r_dy_sq);
+    const double d2x = dv(xp - 2.0 * fc + xm, pc.dx_sq, pc.r_dx_sq);
+    const double d2y = dv(yp - 2.0 * fc + ym, pc.dy_sq, pc.r_dy_sq);
     const double d2z = (zp - 2.0 * fc + zm) * pc.inv_dz2;
     const double visc = pc.nu * (d2x + d2y + d2z);
     const double a = fc + pc.dt * (-conv + visc + src);
@@ -2284,11 +2320,22 @@ static __global__ __launch_bounds__(64 * PR_TY, pred_min_waves<PF>()) void k_pre
 #pragma unroll
         for (int f = 0; f < 3; ++f) {
             const double2 lr = xnbr(z, pc3[f], b.e[f]);
+            // fast divisions, then one wave-uniform check per field: lanes
+            // with a quotient outside divz's range redo the pair with the
+            // generic division (bitwise the same where both apply)
+            double r0, r1;
+            auto compute = [&](auto dv) __attribute__((always_inline)) {
+                r0 = pred_cell(pc, dv, u0, v0, w0, pc3[f].x, lr.x, pc3[f].y, b.ym[f].x,
+                               b.yp[f].x, pm[f].x, b.pp[f].x, s0[f]);
+                r1 = pred_cell(pc, dv, u1, v1, w1, pc3[f].y, pc3[f].x, lr.y, b.ym[f].y,
+                               b.yp[f].y, pm[f].y, b.pp[f].y, s1[f]);
+            };
+            bool ok = true;
+            compute(DivFastZ{ok});
+            if (__builtin_expect(wave_any_bad(ok), 0)) {
+                if (!ok) compute(DivExact{});
+            }
             double2 o = pc3[f];  // boundary cells: u* = u
-            const double r0 = pred_cell(pc, u0, v0, w0, pc3[f].x, lr.x, pc3[f].y, b.ym[f].x,
-                                        b.yp[f].x, pm[f].x, b.pp[f].x, s0[f]);
-            const double r1 = pred_cell(pc, u1, v1, w1, pc3[f].y, pc3[f].x, lr.y, b.ym[f].y,
-                                        b.yp[f].y, pm[f].y, b.pp[f].y, s1[f]);
             if (z.in0) o.x = r0;
             if (z.in1) o.y = r1;
             if (z.xok) st2(O[f], idx, o);
@@ -2337,7 +2384,7 @@ static __global__ __launch_bounds__(256) void k_shell_copy(Geo g, const double* 
 // Corrector (solver_projection.c:230-250) on the interior rows and planes +
 // NaN/Inf scan and max |u|, max |p| of those cells; boundary cells of the
 // tile's rows keep u (== u*) and join the scan. The rest of the shell is
-// scanned by k_shell_stats. red[0] = max |u| (encoded), [1] = max |p|,
+// scanned by k_shell_stats. red[0] = max |u|^2 (encoded), [1] = max |p|,
 // [2] = non-finite flag.
 struct CorrCoef2 {
     double two_dx, two_dy, inv_2dz;
@@ -2374,8 +2421,12 @@ __device__ __forceinline__ void corr_reduce(double mv, double mp, bool bad,
 __device__ __forceinline__ void cell_stats(double u, double v, double w, double p, double& mv,
                                            double& mp, bool& bad) {
     if (!isfinite(u) || !isfinite(v) || !isfinite(w) || !isfinite(p)) bad = true;
-    const double vel = sqrt((u * u) + (v * v) + (w * w));  // solver_registry.c:31-49
-    if (vel > mv) mv = vel;
+    // solver_registry.c:31-49 takes max sqrt(u^2 + v^2 + w^2); sqrt is
+    // correctly rounded, hence monotone, so the maximum of the squared speeds
+    // is reduced (red[0]) and the host takes one sqrt of it: bitwise the same
+    // value, and no fp64 sqrt sequence per cell
+    const double vel2 = (u * u) + (v * v) + (w * w);
+    if (vel2 > mv) mv = vel2;
     const double ap = fabs(p);
     if (ap > mp) mp = ap;
 }
@@ -2418,12 +2469,24 @@ static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
             const double2 lr = xnbr(z, pc, q.e);
             const double left = lr.x, right = lr.y;
             double2 nu = q.a, nv = q.b, nw = q.c;  // boundary cells: u = u* (== u)
+            // fast divisions, one wave-uniform check, generic division for
+            // lanes whose quotients left divz's range (as in k_pred2)
+            double dx0, dy0, dx1, dy1;
+            auto compute = [&](auto dv) __attribute__((always_inline)) {
+                dx0 = dv(pc.y - left, cc.two_dx, cc.r_two_dx);
+                dy0 = dv(q.yp.x - q.ym.x, cc.two_dy, cc.r_two_dy);
+                dx1 = dv(right - pc.x, cc.two_dx, cc.r_two_dx);
+                dy1 = dv(q.yp.y - q.ym.y, cc.two_dy, cc.r_two_dy);
+            };
+            bool ok = true;
+            compute(DivFastZ{ok});
+            if (__builtin_expect(wave_any_bad(ok), 0)) {
+                if (!ok) compute(DivExact{});
+            }
             {
-                const double dp_dx = divz(pc.y - left, cc.two_dx, cc.r_two_dx);
-                const double dp_dy = divz(q.yp.x - q.ym.x, cc.two_dy, cc.r_two_dy);
                 const double dp_dz = (q.pp.x - pm.x) * cc.inv_2dz;
-                const double x0 = fmax(-100.0, fmin(100.0, q.a.x - cc.dt_over_rho * dp_dx));
-                const double y0 = fmax(-100.0, fmin(100.0, q.b.x - cc.dt_over_rho * dp_dy));
+                const double x0 = fmax(-100.0, fmin(100.0, q.a.x - cc.dt_over_rho * dx0));
+                const double y0 = fmax(-100.0, fmin(100.0, q.b.x - cc.dt_over_rho * dy0));
                 const double w0 = fmax(-100.0, fmin(100.0, q.c.x - cc.dt_over_rho * dp_dz));
                 if (z.in0) {
                     nu.x = x0;
@@ -2432,11 +2495,9 @@ static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
                 }
             }
             {
-                const double dp_dx = divz(right - pc.x, cc.two_dx, cc.r_two_dx);
-                const double dp_dy = divz(q.yp.y - q.ym.y, cc.two_dy, cc.r_two_dy);
                 const double dp_dz = (q.pp.y - pm.y) * cc.inv_2dz;
-                const double x1 = fmax(-100.0, fmin(100.0, q.a.y - cc.dt_over_rho * dp_dx));
-                const double y1 = fmax(-100.0, fmin(100.0, q.b.y - cc.dt_over_rho * dp_dy));
+                const double x1 = fmax(-100.0, fmin(100.0, q.a.y - cc.dt_over_rho * dx1));
+                const double y1 = fmax(-100.0, fmin(100.0, q.b.y - cc.dt_over_rho * dy1));
                 const double w1 = fmax(-100.0, fmin(100.0, q.c.y - cc.dt_over_rho * dp_dz));
                 if (z.in1) {
                     nu.y = x1;

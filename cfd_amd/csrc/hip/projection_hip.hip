@@ -811,7 +811,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         pg.tiles_x = (int)((nx + 127) / 128);
         pg.tiles_y = (int)((ny + PR_TY - 1) / PR_TY);
         const long long xy = (long long)pg.tiles_x * pg.tiles_y;
-        const long long zt = std::max(1LL, (8LL * c->grid_cap / 8 + xy - 1) / xy);
+        const long long zt = std::max(1LL, (4LL * c->grid_cap / PR_TY + xy - 1) / xy);
         pg.kc = (int)std::max<long long>(1, (nint_k + zt - 1) / zt);
         pg.tiles_z = (nint_k + pg.kc - 1) / pg.kc;
     }
@@ -1360,7 +1360,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     }
     if (stats) {
         stats->iterations = 1;
-        stats->max_velocity = ord_dec(c->h_red[0]);
+        stats->max_velocity = std::sqrt(ord_dec(c->h_red[0]));  // red[0]: max |u|^2
         stats->max_pressure = ord_dec(c->h_red[1]);
         stats->max_temperature = c->have_T ? c->max_T : 0.0;
     }

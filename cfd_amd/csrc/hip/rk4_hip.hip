@@ -137,7 +137,7 @@ static cfd_status_t rk4_step_impl(hip_proj_ctx* c, const grid* g, const ns_solve
     }
     if (stats) {
         stats->iterations = 1;
-        stats->max_velocity = ord_dec(c->h_red[0]);
+        stats->max_velocity = std::sqrt(ord_dec(c->h_red[0]));  // red[0]: max |u|^2
         stats->max_pressure = ord_dec(c->h_red[1]);
         stats->max_temperature = c->have_T ? c->max_T : 0.0;
     }
