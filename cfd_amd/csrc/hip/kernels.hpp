@@ -2159,6 +2159,9 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
 // nx - 1) are copies; the rest of the boundary shell (rows j = 0, ny - 1, the
 // z faces) is done by k_shell_copy / k_shell_stats.
 // ===========================================================================
+#ifndef CFD_PR_SYNC
+#define CFD_PR_SYNC 1
+#endif
 #ifndef CFD_PR_TY
 #define CFD_PR_TY 4
 #endif
@@ -2269,7 +2272,11 @@ static __global__ __launch_bounds__(64 * PR_TY, pred_min_waves<PF>()) void k_pre
     const double* __restrict__ src_u_row, const double* __restrict__ src_v_col,
     double* __restrict__ us, double* __restrict__ vs, double* __restrict__ ws) {
     const ZTile z = ztile(g);
-    if (z.j < 1 || z.j > g.ny - 2) return;  // boundary rows: k_shell_copy
+    if (z.j < 1 || z.j > g.ny - 2) {  // boundary rows: k_shell_copy
+        if (CFD_PR_SYNC)
+            for (int k = z.kb; k < z.ke; ++k) __syncthreads();
+        return;
+    }
     const double su = src_u_row[z.j];
     const double sv0 = z.xok ? src_v_col[z.i0] : 0.0;
     const double sv1 = z.in1 ? src_v_col[z.i0 + 1] : 0.0;
@@ -2294,6 +2301,7 @@ static __global__ __launch_bounds__(64 * PR_TY, pred_min_waves<PF>()) void k_pre
     }
     // plane k from bundle b; the loads of plane k + 1 go to nb first
     auto step = [&](const PredBundle& b0, PredBundle& nb, int k) __attribute__((always_inline)) {
+        if (CFD_PR_SYNC) __syncthreads();  // keep the tile's waves on one plane
         const long long idx = idx0 + (long long)(k - z.kb) * g.ps;
         PredBundle cur;
         if (PF) {
@@ -2458,6 +2466,7 @@ static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
             q.c = ld2(ws, idx);
         };
         auto step = [&](const CorrBundle& q0, CorrBundle& nq, int k) __attribute__((always_inline)) {
+            if (CFD_PR_SYNC) __syncthreads();  // keep the tile's waves on one plane
             const long long idx = idx0 + (long long)(k - z.kb) * g.ps;
             CorrBundle cur;
             if (PF) {
@@ -2527,6 +2536,8 @@ static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
         } else {
             for (int k = z.kb; k < z.ke; ++k) step(A, B, k);
         }
+    } else if (CFD_PR_SYNC) {
+        for (int k = z.kb; k < z.ke; ++k) __syncthreads();
     }
     corr_reduce(mv, mp, bad, red);
 }
