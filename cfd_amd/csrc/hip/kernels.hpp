@@ -1913,10 +1913,16 @@ constexpr int rb1_oy() { return 1024 / TC - 4; }  // output rows per tile
 //  - rhs is not loaded on the two halo rows, which never use it.
 // PF = the register-ring prefetch below (r02: 0.90 -> 0.76 ms per iteration at
 // 512^3 on one box, 128 VGPRs); the product instantiates PF = true.
-template <int FL, int TC, bool PF>
+// DIST (Z-slabs): R on a halo plane that has a neighbour (rh_lo: plane k0 - 1,
+// rh_hi: plane k1) is the neighbour's R of its edge plane, exchanged into RH
+// beforehand (k_rb_edge_r + halo); it cannot be formed here, since that needs
+// X two planes beyond the halo. The L-inf residual leaves as in k_rx: the
+// device mailbox's max, or dred for an RCCL max all-reduce + k_rx_finish.
+template <int FL, int TC, bool PF, bool DIST = false>
 static __global__ __launch_bounds__(1024, 4) void k_rb1(
     SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
-    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it) {
+    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
+    const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred) {
     constexpr int NW = 16;  // waves
     constexpr int TR = rb1_rows<TC>();
     constexpr int OX = rb1_ox<TC>(), OY = rb1_oy<TC>();
@@ -2035,6 +2041,10 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
         const double2 ryn = lget(rb, q & 1, rhi, c);
         const double rlr = E ? rb[q & 1][r][1][cm] : rb[q & 1][r][0][cp];
         double2 R = xc;
+        if constexpr (DIST) {
+            if ((qa == g.k0 - 1 && rh_lo) || (qa == g.k1 && rh_hi))
+                R = ld2(RH, (long long)qa * g.ps + colx);
+        }
         const double2 ys = lget(xb, qa & 1, rlo, c);
         const double2 yn = lget(xb, qa & 1, rhi, c);
         const double left = xb[qa & 1][r][1][cm];
@@ -2133,7 +2143,42 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
         double tot = 0.0;
         for (int v = 0; v < NW; ++v) tot = fmax(tot, shs[v]);
         __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rx_finish(st, tot, it);
+        if (!DIST) {
+            rx_finish(st, tot, it);
+        } else if (mb) {
+            double gm;
+            if (mbox_allreduce(mb, tot, &gm, true)) {
+                rx_finish(st, gm, it);
+            } else {
+                st->done = 1;
+                st->status = ST_COMM_TIMEOUT;
+            }
+        } else {
+            dred[0] = ord_enc(tot);
+        }
+    }
+}
+
+// R (the first colour SOR-updated, linear_solver_redblack.c:97-114) of a
+// slab's two edge planes k0 and k1 - 1 into RH, for the neighbours' k_rb1
+// (DIST); same operands and order as k_rb1's R, so bitwise equal to it.
+static __global__ __launch_bounds__(256) void k_rb_edge_r(SGeo g, RelaxCoef rc,
+                                                         const double* __restrict__ X,
+                                                         const double* __restrict__ rhs,
+                                                         double* __restrict__ RH) {
+    const long long plane = (long long)g.nx * g.ny;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < 2 * plane;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int k = (e < plane) ? g.k0 : g.k1 - 1;
+        const long long q = e % plane;
+        const int j = (int)(q / g.nx), i = (int)(q % g.nx);
+        if (i < 1 || i > g.nx - 2 || j < 1 || j > g.ny - 2) continue;
+        const long long c = (long long)k * g.ps + (long long)j * g.px + i;
+        double v = X[c];
+        if (((i + j + k + g.kofs) & 1) == 1)
+            v = sor1(rc, DivC{}, X[c], X[c - 1], X[c + 1], X[c - g.px], X[c + g.px], X[c - g.ps],
+                     X[c + g.ps], rhs[c]);
+        RH[c] = v;
     }
 }
 

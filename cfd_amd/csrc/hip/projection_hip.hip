@@ -413,7 +413,10 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     };
     // one-pass RB-SOR (k_rb1) on a single device in 3-D; relax_two_pass = 2
     // forces the two colour sweeps of k_rx
-    const bool single = method == HIP_POISSON_REDBLACK && !D && c->nz > 1 &&
+    // one-pass RB-SOR (k_rb1) in 3-D, on one device or on Z-slabs (there with
+    // the edge planes' R exchanged first); relax_two_pass = 2 forces the two
+    // colour sweeps of k_rx
+    const bool single = method == HIP_POISSON_REDBLACK && c->nz > 1 &&
                         c->cfg.relax_two_pass == 0;
     const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
     ST_TRY(halo(c, {c->pn}));
@@ -425,7 +428,28 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     auto iterate = [&](int it) -> cfd_status_t {
         double* xi = X[it & 1];
         double* xo = X[(it + 1) & 1];
-        if (single) {
+        if (single && D) {
+            // R of the own edge planes -> the neighbours' halo planes of RH
+            // (the CG residual array, free during a relaxation solve), then
+            // the one-pass sweep with R on the halo planes taken from RH
+            double* RH = c->r;
+            c->cg_scratch_dirty = 1;
+            const long long plane = (long long)c->nx * (long long)c->ny;
+            const unsigned ne = (unsigned)std::min<long long>((2 * plane + 255) / 256,
+                                                              (long long)c->grid_cap * 4);
+            timed(c, HIP_KT_RELAX, [&] {
+                hipExtLaunchKernelGGL(k_rb_edge_r, dim3(ne), dim3(256), 0, c->stream, c->ta,
+                                      c->tb, 0, c->rgeo, rc, xi, c->rhs, RH);
+            });
+            ST_TRY(halo(c, {RH}));
+            timed(c, HIP_KT_RELAX, [&] {
+                hipExtLaunchKernelGGL((k_rb1<FL, 64, true, true>), dim3(nb1), dim3(1024), 0,
+                                      c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo, c->rhs,
+                                      c->rxst, c->partials, c->counter, it, (const double*)RH,
+                                      c->geo.lo_face ? 0 : 1, c->geo.hi_face ? 0 : 1, mb, dred);
+            });
+            ST_TRY(finish(it));
+        } else if (single) {
             // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the
             // end-of-step loads (experiments)
             static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
@@ -433,7 +457,8 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
 #define RB1_LAUNCH(TCV, PFV)                                                                   \
     hipExtLaunchKernelGGL((k_rb1<FL, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
                           c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
-                          c->counter, it)
+                          c->counter, it, (const double*)nullptr, 0, 0, (Mbox*)nullptr,        \
+                          (unsigned long long*)nullptr)
             timed(c, HIP_KT_RELAX, [&] {
                 if (!rb1_pf) RB1_LAUNCH(64, false);
                 else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
