@@ -235,12 +235,14 @@ def test_slab_poisson_cg_vs_oracle(hip_lib):
 
 
 @pytest.mark.parametrize("method", [A.HIP_POISSON_REDBLACK, A.HIP_POISSON_JACOBI])
-@pytest.mark.parametrize("nranks,two_pass,maxit", [(4, 0, None), (4, 1, None), (2, 0, None),
-                                                   (3, 0, 11)])
+@pytest.mark.parametrize("nranks,two_pass,maxit", [(4, 0, None), (4, 1, None), (4, 2, None),
+                                                   (2, 0, None), (3, 0, 11)])
 def test_slab_poisson_relax_bitwise(hip_lib, method, nranks, two_pass, maxit):
     """Slab RB-SOR / Jacobi, fused device loop (residual max across ranks) and
     two-pass form: bitwise the oracle, iteration counts and status included;
-    every rank's halo planes end equal to the neighbours' owned planes."""
+    every rank's halo planes end equal to the neighbours' owned planes.
+    RB-SOR: relax_two_pass 0 = one pass per iteration (k_rb_edge_r, R halo,
+    k_rb1<DIST>), 2 = the two colour sweeps of k_rx, 1 = the unfused form."""
     g, rhs = cases.cos_rhs(17)
     xo = np.zeros_like(rhs)
     if maxit is None:
