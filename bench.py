@@ -38,6 +38,7 @@ BYTES_SWEEP_AX = 64.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2};
                         # (the 4 pending alpha p folded; p_{it-1} is sweep A's p_old)
 BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
 BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
+BYTES_CG_SMALL_ITER = 64.0    # small grids, k_cg_small per iteration (x updated every iteration)
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
 BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
 
@@ -195,14 +196,25 @@ def main():
         avg = ms / cnt if cnt else None
         ach = bpc * n_loc / (avg * 1e-3) / 1e9 if cnt else None
         sweeps[key] = (kname, bpc, avg, cnt, ach, ms)
-    if args.cg_variant == 1:  # one iteration = update + SpMV
+    small_ms, small_n = kt.get("cg_small", (0.0, 0))
+    if small_n:
+        # small grids: each solve is ONE persistent launch (k_cg_small) that
+        # moves 64 B/cell per iteration (A: r, p_old -> p; B: p, r, x -> r, x)
+        its_per_launch = sum(iters) / small_n
+        bpc_small = BYTES_CG_SMALL_ITER * its_per_launch
+        avg = small_ms / small_n
+        sweeps["cg_small"] = ("k_cg_small", bpc_small, avg, small_n,
+                              bpc_small * n_loc / (avg * 1e-3) / 1e9, small_ms)
+    if small_n:  # one iteration = the solve's time / its iterations
+        cg_iter_ms = small_ms / max(1, sum(iters))
+    elif args.cg_variant == 1:  # one iteration = update + SpMV
         cg_iter_ms = (sweeps["cc_update"][2] or 0.0) + (sweeps["cc_spmv"][2] or 0.0)
     else:  # one CG iteration = the mean of the two sweep A forms + sweep B
         na = sweeps["cg_sweep_a"][3] + sweeps["cg_sweep_bx"][3]
         avg_a = (sweeps["cg_sweep_a"][5] + sweeps["cg_sweep_bx"][5]) / na if na else 0.0
         cg_iter_ms = avg_a + (sweeps["cg_sweep_b"][2] or 0.0)
     # roofline on the dominant sweep (largest total time)
-    dom = max(sweeps, key=lambda k: sweeps[k][5])
+    dom = max(sweeps, key=lambda k: sweeps[k][5] or 0.0)
     kname, bpc_dom, avg_dom, _, ach_dom, _ = sweeps[dom]
     # measured HBM bytes: the committed PMC profile of THESE kernel sources
     # (2*FETCH_SIZE + WRITE_SIZE per launch) x this run's launch counts

@@ -807,6 +807,156 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Whole CG solve in ONE persistent launch for small grids (r02b). On a
+// 128 x 128 grid a CG iteration's two sweeps cost ~15 us, nearly all kernel
+// dispatch and completion. Here one cooperative launch runs
+// every iteration: phase A (p = r + beta p_old, A p, (p, Ap)), a grid barrier,
+// phase B (x += alpha p, r -= alpha A p, (r, r)), a grid barrier (up to 256
+// workgroups, one per 256 interior cells). Every
+// workgroup sums the per-workgroup partials in the same order and applies
+// the state transition (fin_A / fin_B) to its own LDS copy of the CG state,
+// so all leave the loop at the same iteration with no extra barrier. r and
+// the two p buffers are shared between workgroups inside the launch, so they
+// move through agent-scope atomic loads / stores (coherent across the XCDs'
+// L2s); x is only touched by its own cell. Per-cell arithmetic is the
+// sweeps' (same lap7 operands, p = r + beta p_old, r + (-alpha) A p,
+// x + alpha p per iteration, which is bitwise the sweeps' x fold); only the
+// dot-product summation order differs, as between the sweep kernels and the
+// reference. The barrier wait is bounded (a timeout ends the solve with
+// ST_COMM_TIMEOUT instead of hanging the GPU).
+// ---------------------------------------------------------------------------
+constexpr int CGS_THREADS = 256;
+constexpr int CGS_MAX_WG = 256;
+constexpr long long CG_SMALL_CELLS = 300000;  // default ceiling (interior cells): 64^3 yes, 96^3 no
+
+static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
+                                                                 double* __restrict__ x, double* r,
+                                                                 double* pa, double* pb,
+                                                                 CgState* st, double* partials,
+                                                                 unsigned* bar,
+                                                                 long long timeout_ticks) {
+    __shared__ CgState ls;
+    __shared__ double sh[CGS_THREADS / 64];
+    __shared__ int bad;
+    const unsigned nb = gridDim.x;
+    const long long nxi = g.nx - 2, nyi = g.ny - 2;
+    const long long ncell = nxi * nyi * (long long)(g.k1 - g.k0);
+    if (threadIdx.x == 0) {
+        ls = *st;
+        bad = 0;
+    }
+    __syncthreads();
+    unsigned target = 0;
+    auto barrier = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores landed
+        __syncthreads();
+        target += nb;
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add((gu32*)bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long t0 = wall_clock64();
+            while (__hip_atomic_load((gu32*)bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                   target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > timeout_ticks) {
+                    bad = 1;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    };
+    // block partial -> partials[slot][block] -> barrier -> grid total (thread 0)
+    auto gsum = [&](int slot, double v) __attribute__((always_inline)) {
+        v = wave_sum(v);
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double b = 0.0;
+#pragma unroll
+            for (int w = 0; w < CGS_THREADS / 64; ++w) b += sh[w];
+            store_sc1(&partials[slot * CGS_MAX_WG + blockIdx.x], b);
+        }
+        barrier();
+        // every workgroup: wave w sums partials [64 w, 64 w + 64), then the
+        // wave totals in order (the same fixed tree in every workgroup)
+        double t = (threadIdx.x < nb) ? load_sc1(&partials[slot * CGS_MAX_WG + threadIdx.x]) : 0.0;
+        t = wave_sum(t);
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
+        __syncthreads();
+        double tot = 0.0;
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int w = 0; w < CGS_THREADS / 64; ++w) tot += sh[w];
+        }
+        __syncthreads();  // sh is reused by the next gsum
+        return tot;
+    };
+    auto cell = [&](long long e) __attribute__((always_inline)) {
+        const long long i = 1 + e % nxi;
+        const long long q = e / nxi;
+        const long long j = 1 + q % nyi;
+        const long long k = g.k0 + q / nyi;
+        return k * g.ps + j * g.px + i;
+    };
+    const long long stride = (long long)nb * CGS_THREADS;
+    for (int it = 0;; ++it) {
+        if (ls.done) break;
+        double* pn = (it & 1) ? pb : pa;
+        const double* po = (it & 1) ? pa : pb;
+        const bool first = (it == 0);
+        const double beta = first ? 0.0 : ls.beta;
+        // phase A: p_it = r + beta p_{it-1} (formed at the neighbours too), (p, A p)
+        double acc = 0.0;
+        for (long long e = (long long)blockIdx.x * CGS_THREADS + threadIdx.x; e < ncell;
+             e += stride) {
+            const long long c = cell(e);
+            auto P = [&](long long q) __attribute__((always_inline)) {
+                const double rv = load_sc1(&r[q]);
+                return first ? rv : rv + beta * load_sc1(&po[q]);
+            };
+            const double pc = P(c);
+            const double Ap = -lap7(L, pc, P(c - 1), P(c + 1), P(c - g.px), P(c + g.px),
+                                    P(c - g.sz), P(c + g.sz));
+            store_sc1(&pn[c], pc);
+            acc += pc * Ap;
+        }
+        const double tA = gsum(0, acc);
+        if (bad) break;
+        if (threadIdx.x == 0) fin_A(&ls, tA, it);
+        __syncthreads();
+        if (ls.done) break;
+        // phase B: x += alpha p, r -= alpha A p (A p recomputed), (r, r)
+        const double al = ls.alpha[it % CG_XFOLD];
+        const double ma = -al;
+        acc = 0.0;
+        for (long long e = (long long)blockIdx.x * CGS_THREADS + threadIdx.x; e < ncell;
+             e += stride) {
+            const long long c = cell(e);
+            const double pc = load_sc1(&pn[c]);
+            const double Ap = -lap7(L, pc, load_sc1(&pn[c - 1]), load_sc1(&pn[c + 1]),
+                                    load_sc1(&pn[c - g.px]), load_sc1(&pn[c + g.px]),
+                                    load_sc1(&pn[c - g.sz]), load_sc1(&pn[c + g.sz]));
+            x[c] = x[c] + al * pc;
+            const double rn = load_sc1(&r[c]) + ma * Ap;
+            store_sc1(&r[c], rn);
+            acc += rn * rn;
+        }
+        const double tB = gsum(1, acc);
+        if (bad) break;
+        if (threadIdx.x == 0) fin_B(&ls, tB, it);
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (bad) {
+            ls.done = 1;
+            ls.status = ST_COMM_TIMEOUT;
+        }
+        ls.xdone = ls.nalpha;  // x holds every alpha_j p_j: nothing for k_cg_finalize
+        *st = ls;
+    }
+}
+
 // Apply the x += alpha_j p_j the sweeps have not folded yet (j in [xdone,
 // nalpha), at most CG_XFOLD - 1 of them), in order, partial sums in a register
 // (bitwise the reference's sequential updates).

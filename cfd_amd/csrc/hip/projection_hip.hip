@@ -281,8 +281,43 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         ST_TRY(reduce_cc(-1, true));
     }
     auto step_it = [&](int it) { return cc ? iterate_cc(it) : iterate(it); };
+    // small grids: the whole solve in one cooperative launch (k_cg_small);
+    // CFD_HIP_CG_SMALL = 0 never, 1 up to 64 x 256 x 16 interior cells,
+    // default up to CG_SMALL_CELLS
+    bool small_done = false;
+    const long long ncell = (long long)(c->nx - 2) * (long long)(c->ny - 2) *
+                            (long long)(c->geo.k1 - c->geo.k0);
+    {
+        const char* e = getenv("CFD_HIP_CG_SMALL");
+        const int mode = e ? atoi(e) : -1;
+        const long long cap = (mode == 1) ? (long long)CGS_MAX_WG * CGS_THREADS * 16
+                                          : (mode == 0 ? 0 : CG_SMALL_CELLS);
+        if (!D && !cc && max_iter > 0 && ncell > 0 && ncell <= cap) {
+            int rate_khz = 0;
+            hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->device);
+            long long ticks = (long long)std::max(rate_khz, 1000) * 1000LL * 20;  // 20 s
+            unsigned nbw = (unsigned)std::min<long long>(
+                CGS_MAX_WG, (ncell + CGS_THREADS - 1) / CGS_THREADS);
+            Geo geo = c->geo;
+            Lap lap = L;
+            double* xx = x;
+            unsigned* barp = c->counter + 8;
+            void* args[] = {&geo, &lap, &xx, &c->r, &c->pa, &c->pb, &c->st, &c->partials,
+                            &barp, &ticks};
+            ST_TRY(timed_span(c, c->stream, HIP_KT_CG_SMALL, [&]() -> cfd_status_t {
+                HIP_TRY(hipMemsetAsync(barp, 0, sizeof(unsigned), c->stream));
+                if (hipLaunchCooperativeKernel((const void*)k_cg_small, dim3(nbw),
+                                               dim3(CGS_THREADS), args, 0,
+                                               c->stream) == hipSuccess)
+                    small_done = true;
+                else
+                    (void)hipGetLastError();  // not co-resident here: the sweep loop
+                return CFD_SUCCESS;
+            }));
+        }
+    }
     int it = 0;
-    if (max_iter > 0) {
+    if (max_iter > 0 && !small_done) {
         ST_TRY(step_it(0));
         it = 1;
     }
@@ -292,7 +327,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     int chunk = 8;
     const int chunk_max = std::max(1, c->cfg.poll_interval);
     int slot = 0, prev = -1;
-    while (it < max_iter) {
+    while (it < max_iter && !small_done) {
         const int n = std::min(chunk, max_iter - it);
         for (int q = 0; q < n; ++q, ++it) ST_TRY(step_it(it));
         HIP_TRY(hipMemcpyAsync(&c->h_state[slot], c->st, sizeof(CgState), hipMemcpyDeviceToHost,
@@ -789,12 +824,15 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         sg.kc = c->cfg.kchunk;
     } else {
         // long z runs (each chunk re-reads two planes), shortened (down to
-        // 16) until every CU has a workgroup: a thin slab must still fill
-        // all 256 CUs. r01f at 512^3: 256-plane runs (256 workgroups) beat
-        // 64 by ~2 %; one 8-rank slab: 32 beat 16 (profiles/r01f_sweep_*)
+        // 4) until every CU has a workgroup: a thin slab or a mid-size grid
+        // must still fill all 256 CUs. r01f at 512^3: 256-plane runs (256
+        // workgroups) beat 64 by ~2 %; one 8-rank slab: 32 beat 16
+        // (profiles/r01f_sweep_*). r02b: the floor was 16, which left 96^3 /
+        // 128^3 at 36 / 64 workgroups; 4 takes a CG iteration from 53 to
+        // 25 us / 58 to 33 us there (profiles/r02_small_grids.jsonl)
         sg.kc = 256;
         const long long want = c->grid_cap / 8;
-        while (sg.kc > 16 &&
+        while (sg.kc > 4 &&
                (long long)sg.tiles_x * sg.tiles_y * ((nint_k + sg.kc - 1) / sg.kc) < want)
             sg.kc /= 2;
     }

@@ -135,7 +135,8 @@ typedef enum {
     HIP_KT_HALO = 12,      /* Z-slabs: CG halo exchange (span on its stream) */
     HIP_KT_ALLREDUCE = 13, /* Z-slabs: RCCL all-reduce of a CG dot (+ finish kernel); the
                               device-mailbox reduction runs inside the sweep instead */
-    HIP_KT_COUNT = 14
+    HIP_KT_CG_SMALL = 14,  /* small grids: the whole CG solve in one cooperative launch */
+    HIP_KT_COUNT = 15
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);

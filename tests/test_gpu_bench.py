@@ -4,7 +4,6 @@ CFD_BENCH_SHARED_GPU: every rank on device 0, RCCL over its socket
 transport). The 8-GPU run itself is the driver's."""
 import json
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -16,12 +15,6 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
         "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
-
-
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _last_json(out):
@@ -61,8 +54,11 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
     launch (here 128 interior planes = 16 per rank)."""
     env = _env()
     env["CFD_BENCH_SHARED_GPU"] = "1"
+    # c10d rendezvous on port 0: the agent binds a free port itself (a port
+    # probed free here can be taken before torchrun binds it: EADDRINUSE)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", str(world),
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
+           "bench.py", "--gpus", str(world),
            "--size", str(size), "--steps", "2", "--warmup", "1", "--case", case]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]

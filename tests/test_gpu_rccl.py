@@ -1,6 +1,5 @@
 """The Z-slab path over RCCL with two processes (tests/rccl_slab_worker.py)."""
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -10,12 +9,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parent.parent
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 @pytest.mark.parametrize("world,device_allreduce", [(2, "0"), (2, "1"), (4, "1")])
@@ -29,7 +22,7 @@ def test_rccl_slabs(hip_lib, world, device_allreduce):
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
            str(ROOT / "tests" / "rccl_slab_worker.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     out = r.stdout + r.stderr
