@@ -863,6 +863,13 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         while (rg.kc > 16 &&
                (long long)rg.tiles_x * rg.tiles_y * ((nint_k + rg.kc - 1) / rg.kc) < 512)
             rg.kc /= 2;
+        // small grids: shorter runs (each costs a two-plane prologue) only
+        // while fewer than half the CUs have a workgroup (r02b: 96^3 31 ->
+        // 17 us per iteration at 4 planes; 128^3, 176 workgroups at 16
+        // planes, is slower at 8 or 4; profiles/r02_small_grids.jsonl)
+        while (rg.kc > 4 &&
+               (long long)rg.tiles_x * rg.tiles_y * ((nint_k + rg.kc - 1) / rg.kc) < 128)
+            rg.kc /= 2;
         rg.kc = std::max(1, std::min(rg.kc, nint_k));
         rg.tiles_z = (nint_k + rg.kc - 1) / rg.kc;
         n_partials = std::max(n_partials, rg.tiles_x * rg.tiles_y * rg.tiles_z);
