@@ -351,7 +351,9 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     const CgState& s = c->h_state[2];
     flush_timing(c, s.iterations);
     if (s.status == ST_COMM_TIMEOUT) {
-        set_err(CFD_ERROR, "projection_hip: slab all-reduce timed out (a rank stopped)");
+        set_err(CFD_ERROR, small_done
+                               ? "projection_hip: small-grid CG grid barrier timed out"
+                               : "projection_hip: slab all-reduce timed out (a rank stopped)");
         return CFD_ERROR;
     }
     const bool stagnated = (s.status == ST_STAGNATED);
