@@ -1468,6 +1468,69 @@ struct Fld4 {
 
 __device__ __forceinline__ double clampl(double x, double lim) { return fmax(-lim, fmin(lim, x)); }
 
+// One cell's RHS (ns_momentum_rhs_scalar.h:49-190 operation order): the 7
+// values of u, v, w, p around the cell (periodic neighbour indices already
+// resolved), rho, dx[i], dy[j], the source-table entries and T; kr = 0 where
+// the reference skips the cell (rho or a spacing below 1e-10).
+struct RkNbr {
+    double c[4], l[4], r[4], d[4], u[4], m[4], p[4];  // centre, x-, x+, y-, y+, z-, z+
+};
+
+template <bool BUOY>
+__device__ __forceinline__ void rk_rhs(const RkCoef& rc, const RkNbr& n, double r, double dxi,
+                                       double dyj, double su, double sv, double Tc,
+                                       double (&kr)[4]) {
+    if (!(r <= 1e-10) && !(fabs(dxi) < 1e-10) && !(fabs(dyj) < 1e-10)) {
+        const double tdx = 2.0 * dxi, tdy = 2.0 * dyj;
+        const double dxx = dxi * dxi, dyy = dyj * dyj;
+        const double uc = n.c[0], vc = n.c[1], wc = n.c[2];
+        double du_dx = (n.r[0] - n.l[0]) / tdx, du_dy = (n.u[0] - n.d[0]) / tdy;
+        double du_dz = (n.p[0] - n.m[0]) * rc.inv_2dz;
+        double dv_dx = (n.r[1] - n.l[1]) / tdx, dv_dy = (n.u[1] - n.d[1]) / tdy;
+        double dv_dz = (n.p[1] - n.m[1]) * rc.inv_2dz;
+        double dw_dx = (n.r[2] - n.l[2]) / tdx, dw_dy = (n.u[2] - n.d[2]) / tdy;
+        double dw_dz = (n.p[2] - n.m[2]) * rc.inv_2dz;
+        double dp_dx = (n.r[3] - n.l[3]) / tdx, dp_dy = (n.u[3] - n.d[3]) / tdy;
+        double dp_dz = (n.p[3] - n.m[3]) * rc.inv_2dz;
+        double d2u_dx2 = (n.r[0] - 2.0 * uc + n.l[0]) / dxx;
+        double d2u_dy2 = (n.u[0] - 2.0 * uc + n.d[0]) / dyy;
+        double d2u_dz2 = (n.p[0] - 2.0 * uc + n.m[0]) * rc.inv_dz2;
+        double d2v_dx2 = (n.r[1] - 2.0 * vc + n.l[1]) / dxx;
+        double d2v_dy2 = (n.u[1] - 2.0 * vc + n.d[1]) / dyy;
+        double d2v_dz2 = (n.p[1] - 2.0 * vc + n.m[1]) * rc.inv_dz2;
+        double d2w_dx2 = (n.r[2] - 2.0 * wc + n.l[2]) / dxx;
+        double d2w_dy2 = (n.u[2] - 2.0 * wc + n.d[2]) / dyy;
+        double d2w_dz2 = (n.p[2] - 2.0 * wc + n.m[2]) * rc.inv_dz2;
+        double nu = rc.mu / fmax(r, 1e-10);
+        nu = fmin(nu, 1.0);
+        du_dx = clampl(du_dx, 100.0); du_dy = clampl(du_dy, 100.0); du_dz = clampl(du_dz, 100.0);
+        dv_dx = clampl(dv_dx, 100.0); dv_dy = clampl(dv_dy, 100.0); dv_dz = clampl(dv_dz, 100.0);
+        dw_dx = clampl(dw_dx, 100.0); dw_dy = clampl(dw_dy, 100.0); dw_dz = clampl(dw_dz, 100.0);
+        dp_dx = clampl(dp_dx, 100.0); dp_dy = clampl(dp_dy, 100.0); dp_dz = clampl(dp_dz, 100.0);
+        d2u_dx2 = clampl(d2u_dx2, 1000.0); d2u_dy2 = clampl(d2u_dy2, 1000.0);
+        d2u_dz2 = clampl(d2u_dz2, 1000.0); d2v_dx2 = clampl(d2v_dx2, 1000.0);
+        d2v_dy2 = clampl(d2v_dy2, 1000.0); d2v_dz2 = clampl(d2v_dz2, 1000.0);
+        d2w_dx2 = clampl(d2w_dx2, 1000.0); d2w_dy2 = clampl(d2w_dy2, 1000.0);
+        d2w_dz2 = clampl(d2w_dz2, 1000.0);
+        double sw = 0.0;
+        if (BUOY) {
+            const double dT = Tc - rc.T_ref;
+            su += -rc.beta * dT * rc.g0;
+            sv += -rc.beta * dT * rc.g1;
+            sw += -rc.beta * dT * rc.g2;
+        }
+        kr[0] = -uc * du_dx - vc * du_dy - wc * du_dz - dp_dx / r +
+                nu * (d2u_dx2 + d2u_dy2 + d2u_dz2) + su;
+        kr[1] = -uc * dv_dx - vc * dv_dy - wc * dv_dz - dp_dy / r +
+                nu * (d2v_dx2 + d2v_dy2 + d2v_dz2) + sv;
+        kr[2] = -uc * dw_dx - vc * dw_dy - wc * dw_dz - dp_dz / r +
+                nu * (d2w_dx2 + d2w_dy2 + d2w_dz2) + sw;
+        double div = du_dx + dv_dy + dw_dz;
+        div = fmax(-10.0, fmin(10.0, div));
+        kr[3] = -0.1 * r * div;
+    }
+}
+
 template <int STAGE, bool BUOY>
 __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
                                                   Fld4 out, const double* __restrict__ rho,
@@ -1485,70 +1548,28 @@ __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fl
                            k >= g.k0 && k < g.k1);
     double kr[4] = {0.0, 0.0, 0.0, 0.0};
     if (interior) {
-        const double r = rho[idx];
-        const double dxi = dxa[i], dyj = dya[j];
-        if (!(r <= 1e-10) && !(fabs(dxi) < 1e-10) && !(fabs(dyj) < 1e-10)) {
-            const long long il = (i > 1) ? idx - 1 : cidx(g, g.nx - 2, j, k);
-            const long long ir = (i < g.nx - 2) ? idx + 1 : cidx(g, 1, j, k);
-            const long long jd = (j > 1) ? idx - g.px : cidx(g, i, g.ny - 2, k);
-            const long long ju = (j < g.ny - 2) ? idx + g.px : cidx(g, i, 1, k);
-            long long kd = idx, ku = idx;   // 2-D: z terms vanish (stride 0)
-            if (g.sz) {
-                kd = (k > 1) ? idx - g.sz : cidx(g, i, j, g.nz - 2);
-                ku = (k < g.nz - 2) ? idx + g.sz : cidx(g, i, j, 1);
-            }
-            const double* U = cur.f[0];
-            const double* V = cur.f[1];
-            const double* W = cur.f[2];
-            const double* P = cur.f[3];
-            const double tdx = 2.0 * dxi, tdy = 2.0 * dyj;
-            const double dxx = dxi * dxi, dyy = dyj * dyj;
-            const double uc = U[idx], vc = V[idx], wc = W[idx];
-            double du_dx = (U[ir] - U[il]) / tdx, du_dy = (U[ju] - U[jd]) / tdy;
-            double du_dz = (U[ku] - U[kd]) * rc.inv_2dz;
-            double dv_dx = (V[ir] - V[il]) / tdx, dv_dy = (V[ju] - V[jd]) / tdy;
-            double dv_dz = (V[ku] - V[kd]) * rc.inv_2dz;
-            double dw_dx = (W[ir] - W[il]) / tdx, dw_dy = (W[ju] - W[jd]) / tdy;
-            double dw_dz = (W[ku] - W[kd]) * rc.inv_2dz;
-            double dp_dx = (P[ir] - P[il]) / tdx, dp_dy = (P[ju] - P[jd]) / tdy;
-            double dp_dz = (P[ku] - P[kd]) * rc.inv_2dz;
-            double d2u_dx2 = (U[ir] - 2.0 * uc + U[il]) / dxx;
-            double d2u_dy2 = (U[ju] - 2.0 * uc + U[jd]) / dyy;
-            double d2u_dz2 = (U[ku] - 2.0 * uc + U[kd]) * rc.inv_dz2;
-            double d2v_dx2 = (V[ir] - 2.0 * vc + V[il]) / dxx;
-            double d2v_dy2 = (V[ju] - 2.0 * vc + V[jd]) / dyy;
-            double d2v_dz2 = (V[ku] - 2.0 * vc + V[kd]) * rc.inv_dz2;
-            double d2w_dx2 = (W[ir] - 2.0 * wc + W[il]) / dxx;
-            double d2w_dy2 = (W[ju] - 2.0 * wc + W[jd]) / dyy;
-            double d2w_dz2 = (W[ku] - 2.0 * wc + W[kd]) * rc.inv_dz2;
-            double nu = rc.mu / fmax(r, 1e-10);
-            nu = fmin(nu, 1.0);
-            du_dx = clampl(du_dx, 100.0); du_dy = clampl(du_dy, 100.0); du_dz = clampl(du_dz, 100.0);
-            dv_dx = clampl(dv_dx, 100.0); dv_dy = clampl(dv_dy, 100.0); dv_dz = clampl(dv_dz, 100.0);
-            dw_dx = clampl(dw_dx, 100.0); dw_dy = clampl(dw_dy, 100.0); dw_dz = clampl(dw_dz, 100.0);
-            dp_dx = clampl(dp_dx, 100.0); dp_dy = clampl(dp_dy, 100.0); dp_dz = clampl(dp_dz, 100.0);
-            d2u_dx2 = clampl(d2u_dx2, 1000.0); d2u_dy2 = clampl(d2u_dy2, 1000.0);
-            d2u_dz2 = clampl(d2u_dz2, 1000.0); d2v_dx2 = clampl(d2v_dx2, 1000.0);
-            d2v_dy2 = clampl(d2v_dy2, 1000.0); d2v_dz2 = clampl(d2v_dz2, 1000.0);
-            d2w_dx2 = clampl(d2w_dx2, 1000.0); d2w_dy2 = clampl(d2w_dy2, 1000.0);
-            d2w_dz2 = clampl(d2w_dz2, 1000.0);
-            double su = su_row[j], sv = sv_col[i], sw = 0.0;
-            if (BUOY) {
-                const double dT = T[idx] - rc.T_ref;
-                su += -rc.beta * dT * rc.g0;
-                sv += -rc.beta * dT * rc.g1;
-                sw += -rc.beta * dT * rc.g2;
-            }
-            kr[0] = -uc * du_dx - vc * du_dy - wc * du_dz - dp_dx / r +
-                    nu * (d2u_dx2 + d2u_dy2 + d2u_dz2) + su;
-            kr[1] = -uc * dv_dx - vc * dv_dy - wc * dv_dz - dp_dy / r +
-                    nu * (d2v_dx2 + d2v_dy2 + d2v_dz2) + sv;
-            kr[2] = -uc * dw_dx - vc * dw_dy - wc * dw_dz - dp_dz / r +
-                    nu * (d2w_dx2 + d2w_dy2 + d2w_dz2) + sw;
-            double div = du_dx + dv_dy + dw_dz;
-            div = fmax(-10.0, fmin(10.0, div));
-            kr[3] = -0.1 * r * div;
+        const long long il = (i > 1) ? idx - 1 : cidx(g, g.nx - 2, j, k);
+        const long long ir = (i < g.nx - 2) ? idx + 1 : cidx(g, 1, j, k);
+        const long long jd = (j > 1) ? idx - g.px : cidx(g, i, g.ny - 2, k);
+        const long long ju = (j < g.ny - 2) ? idx + g.px : cidx(g, i, 1, k);
+        long long kd = idx, ku = idx;   // 2-D: z terms vanish (stride 0)
+        if (g.sz) {
+            kd = (k > 1) ? idx - g.sz : cidx(g, i, j, g.nz - 2);
+            ku = (k < g.nz - 2) ? idx + g.sz : cidx(g, i, j, 1);
         }
+        RkNbr n;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            n.c[f] = cur.f[f][idx];
+            n.l[f] = cur.f[f][il];
+            n.r[f] = cur.f[f][ir];
+            n.d[f] = cur.f[f][jd];
+            n.u[f] = cur.f[f][ju];
+            n.m[f] = cur.f[f][kd];
+            n.p[f] = cur.f[f][ku];
+        }
+        rk_rhs<BUOY>(rc, n, rho[idx], dxa[i], dya[j], su_row[j], sv_col[i],
+                     BUOY ? T[idx] : 0.0, kr);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1564,6 +1585,87 @@ __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fl
         }
         if (q < 3) o = fmax(-100.0, fmin(100.0, o));
         out.f[q][idx] = o;
+    }
+}
+
+// The same stage on x pairs (r02b): each lane owns cells (i0, i0 + 1) and
+// moves every field with 16-B loads / stores; the cell's x neighbours are the
+// pair's other cell or one scalar load (the periodic indices of i = 1 and
+// nx - 2 by address), y / z neighbours are pair loads of the (periodically
+// resolved) neighbour row / plane. Half the load instructions of k_rk_stage;
+// rk_rhs is shared, so the values are bitwise the per-cell kernel's.
+template <int STAGE, bool BUOY>
+__global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
+                                                   Fld4 out, const double* __restrict__ rho,
+                                                   const double* __restrict__ T,
+                                                   const double* __restrict__ dxa,
+                                                   const double* __restrict__ dya,
+                                                   const double* __restrict__ su_row,
+                                                   const double* __restrict__ sv_col) {
+    const int i0 = blockIdx.x * 128 + 2 * (threadIdx.x & 63);
+    const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.z;
+    if (i0 >= g.nx || j >= g.ny) return;
+    const long long idx = cidx(g, i0, j, k);
+    const bool rowin = (j >= 1 && j <= g.ny - 2 && k >= g.k0 && k < g.k1);
+    const bool ina = rowin && i0 >= 1 && i0 <= g.nx - 2;
+    const bool inb = rowin && i0 + 1 <= g.nx - 2;
+    double kra[4] = {0.0, 0.0, 0.0, 0.0}, krb[4] = {0.0, 0.0, 0.0, 0.0};
+    if (ina || inb) {
+        const long long row = idx - i0;
+        const long long jd = (j > 1) ? idx - g.px : cidx(g, i0, g.ny - 2, k);
+        const long long ju = (j < g.ny - 2) ? idx + g.px : cidx(g, i0, 1, k);
+        long long kd = idx, ku = idx;  // 2-D: z terms vanish (stride 0)
+        if (g.sz) {
+            kd = (k > 1) ? idx - g.sz : cidx(g, i0, j, g.nz - 2);
+            ku = (k < g.nz - 2) ? idx + g.sz : cidx(g, i0, j, 1);
+        }
+        // x neighbours outside the pair: left of i0, right of i0 + 1
+        const long long la = (i0 > 1) ? idx - 1 : row + (g.nx - 2);
+        const long long rb = (i0 + 1 < g.nx - 2) ? idx + 2 : row + 1;
+        RkNbr a, b;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const double* F = cur.f[f];
+            const double2 c2 = ld2(F, idx), d2 = ld2(F, jd), u2 = ld2(F, ju);
+            const double2 m2 = ld2(F, kd), p2 = ld2(F, ku);
+            const double xl = F[la], xr = F[rb];
+            a.c[f] = c2.x; b.c[f] = c2.y;
+            a.d[f] = d2.x; b.d[f] = d2.y;
+            a.u[f] = u2.x; b.u[f] = u2.y;
+            a.m[f] = m2.x; b.m[f] = m2.y;
+            a.p[f] = p2.x; b.p[f] = p2.y;
+            a.l[f] = xl;
+            a.r[f] = (i0 < g.nx - 2) ? c2.y : F[row + 1];  // i0 = nx - 2: periodic
+            b.l[f] = (i0 + 1 > 1) ? c2.x : F[row + (g.nx - 2)];  // i0 + 1 = 1: periodic
+            b.r[f] = xr;
+        }
+        const double2 r2 = ld2(rho, idx);
+        const double2 t2 = BUOY ? ld2(T, idx) : make_double2(0.0, 0.0);
+        const double dyj = dya[j], su = su_row[j];
+        if (ina) rk_rhs<BUOY>(rc, a, r2.x, dxa[i0], dyj, su, sv_col[i0], t2.x, kra);
+        if (inb) rk_rhs<BUOY>(rc, b, r2.y, dxa[i0 + 1], dyj, su, sv_col[i0 + 1], t2.y, krb);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double2 q02 = ld2(q0.f[q], idx);
+        double2 o;
+        if (STAGE == 0) {
+            st2(acc.f[q], idx, make_double2(kra[q], krb[q]));
+            o = make_double2(q02.x + rc.fac * kra[q], q02.y + rc.fac * krb[q]);
+        } else if (STAGE < 3) {
+            const double2 a2 = ld2(acc.f[q], idx);
+            st2(acc.f[q], idx, make_double2(a2.x + 2.0 * kra[q], a2.y + 2.0 * krb[q]));
+            o = make_double2(q02.x + rc.fac * kra[q], q02.y + rc.fac * krb[q]);
+        } else {
+            const double2 a2 = ld2(acc.f[q], idx);
+            o = make_double2(q02.x + rc.fac * (a2.x + kra[q]), q02.y + rc.fac * (a2.y + krb[q]));
+        }
+        if (q < 3) {
+            o.x = fmax(-100.0, fmin(100.0, o.x));
+            o.y = fmax(-100.0, fmin(100.0, o.y));
+        }
+        st2(out.f[q], idx, o);
     }
 }
 

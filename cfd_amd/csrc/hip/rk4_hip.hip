@@ -36,6 +36,21 @@ static cfd_status_t ensure_rk(hip_proj_ctx* c) {
 template <int S>
 static void launch_stage(hip_proj_ctx* c, bool buoy, const RkCoef& rc, const Fld4& cur,
                          const Fld4& q0, const Fld4& acc, const Fld4& out) {
+    // x-pair stage kernel (default); CFD_HIP_RK_PAIR=0 selects the per-cell one
+    static const bool pair = !(getenv("CFD_HIP_RK_PAIR") && atoi(getenv("CFD_HIP_RK_PAIR")) == 0);
+    if (pair) {
+        const dim3 g2((unsigned)((c->nx + 127) / 128), (unsigned)((c->ny + 3) / 4),
+                      (unsigned)c->nz);
+        if (buoy)
+            hipExtLaunchKernelGGL((k_rk_stage2<S, true>), g2, dim3(256), 0, c->stream, c->ta,
+                                  c->tb, 0, c->geo, rc, cur, q0, acc, out, c->rho, c->T, c->dxa,
+                                  c->dya, c->src_u_row, c->src_v_col);
+        else
+            hipExtLaunchKernelGGL((k_rk_stage2<S, false>), g2, dim3(256), 0, c->stream, c->ta,
+                                  c->tb, 0, c->geo, rc, cur, q0, acc, out, c->rho, c->T, c->dxa,
+                                  c->dya, c->src_u_row, c->src_v_col);
+        return;
+    }
     const dim3 grid = cell_grid(c);
     if (buoy)
         hipExtLaunchKernelGGL((k_rk_stage<S, true>), grid, dim3(256), 0, c->stream, c->ta, c->tb,
