@@ -1623,28 +1623,81 @@ __global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, F
         // x neighbours outside the pair: left of i0, right of i0 + 1
         const long long la = (i0 > 1) ? idx - 1 : row + (g.nx - 2);
         const long long rb = (i0 + 1 < g.nx - 2) ? idx + 2 : row + 1;
-        RkNbr a, b;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
+        // one field at a time (p first: its gradient enters u, v, w), so only
+        // one field's neighbourhood is live: same expressions as rk_rhs
+        const double2 r2 = ld2(rho, idx);
+        const double2 t2 = BUOY ? ld2(T, idx) : make_double2(0.0, 0.0);
+        const double dyj = dya[j], su = su_row[j];
+        const double dxa0 = dxa[i0], dxa1 = dxa[min(i0 + 1, g.nx - 1)];
+        const bool oka = ina && !(r2.x <= 1e-10) && !(fabs(dxa0) < 1e-10) && !(fabs(dyj) < 1e-10);
+        const bool okb = inb && !(r2.y <= 1e-10) && !(fabs(dxa1) < 1e-10) && !(fabs(dyj) < 1e-10);
+        const double2 uc = ld2(cur.f[0], idx), vc = ld2(cur.f[1], idx), wc = ld2(cur.f[2], idx);
+        struct D1 { double dx, dy, dz, xx, yy, zz; };
+        // first and second differences of field f at both cells
+        auto diffs = [&](int f, D1& da, D1& db) __attribute__((always_inline)) {
             const double* F = cur.f[f];
             const double2 c2 = ld2(F, idx), d2 = ld2(F, jd), u2 = ld2(F, ju);
             const double2 m2 = ld2(F, kd), p2 = ld2(F, ku);
             const double xl = F[la], xr = F[rb];
-            a.c[f] = c2.x; b.c[f] = c2.y;
-            a.d[f] = d2.x; b.d[f] = d2.y;
-            a.u[f] = u2.x; b.u[f] = u2.y;
-            a.m[f] = m2.x; b.m[f] = m2.y;
-            a.p[f] = p2.x; b.p[f] = p2.y;
-            a.l[f] = xl;
-            a.r[f] = (i0 < g.nx - 2) ? c2.y : F[row + 1];  // i0 = nx - 2: periodic
-            b.l[f] = (i0 + 1 > 1) ? c2.x : F[row + (g.nx - 2)];  // i0 + 1 = 1: periodic
-            b.r[f] = xr;
+            const double ar = (i0 < g.nx - 2) ? c2.y : F[row + 1];
+            const double bl = (i0 + 1 > 1) ? c2.x : F[row + (g.nx - 2)];
+            const double tdxa = 2.0 * dxa0, tdxb = 2.0 * dxa1, tdy = 2.0 * dyj;
+            const double dxxa = dxa0 * dxa0, dxxb = dxa1 * dxa1, dyy = dyj * dyj;
+            da.dx = (ar - xl) / tdxa;
+            da.dy = (u2.x - d2.x) / tdy;
+            da.dz = (p2.x - m2.x) * rc.inv_2dz;
+            da.xx = (ar - 2.0 * c2.x + xl) / dxxa;
+            da.yy = (u2.x - 2.0 * c2.x + d2.x) / dyy;
+            da.zz = (p2.x - 2.0 * c2.x + m2.x) * rc.inv_dz2;
+            db.dx = (xr - bl) / tdxb;
+            db.dy = (u2.y - d2.y) / tdy;
+            db.dz = (p2.y - m2.y) * rc.inv_2dz;
+            db.xx = (xr - 2.0 * c2.y + bl) / dxxb;
+            db.yy = (u2.y - 2.0 * c2.y + d2.y) / dyy;
+            db.zz = (p2.y - 2.0 * c2.y + m2.y) * rc.inv_dz2;
+        };
+        D1 pa_, pb_;
+        diffs(3, pa_, pb_);
+        const double dpxa = clampl(pa_.dx, 100.0), dpya = clampl(pa_.dy, 100.0),
+                     dpza = clampl(pa_.dz, 100.0);
+        const double dpxb = clampl(pb_.dx, 100.0), dpyb = clampl(pb_.dy, 100.0),
+                     dpzb = clampl(pb_.dz, 100.0);
+        const double nua = fmin(rc.mu / fmax(r2.x, 1e-10), 1.0);
+        const double nub = fmin(rc.mu / fmax(r2.y, 1e-10), 1.0);
+        double sa[3] = {su, sv_col[i0], 0.0};
+        double sb[3] = {su, sv_col[min(i0 + 1, g.nx - 1)], 0.0};
+        if (BUOY) {
+            const double dTa = t2.x - rc.T_ref, dTb = t2.y - rc.T_ref;
+            sa[0] += -rc.beta * dTa * rc.g0;
+            sa[1] += -rc.beta * dTa * rc.g1;
+            sa[2] += -rc.beta * dTa * rc.g2;
+            sb[0] += -rc.beta * dTb * rc.g0;
+            sb[1] += -rc.beta * dTb * rc.g1;
+            sb[2] += -rc.beta * dTb * rc.g2;
         }
-        const double2 r2 = ld2(rho, idx);
-        const double2 t2 = BUOY ? ld2(T, idx) : make_double2(0.0, 0.0);
-        const double dyj = dya[j], su = su_row[j];
-        if (ina) rk_rhs<BUOY>(rc, a, r2.x, dxa[i0], dyj, su, sv_col[i0], t2.x, kra);
-        if (inb) rk_rhs<BUOY>(rc, b, r2.y, dxa[i0 + 1], dyj, su, sv_col[i0 + 1], t2.y, krb);
+        const double gpa[3] = {dpxa, dpya, dpza}, gpb[3] = {dpxb, dpyb, dpzb};
+        double diva = 0.0, divb = 0.0;  // du_dx + dv_dy + dw_dz (clamped terms)
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            D1 da, db;
+            diffs(f, da, db);
+            da.dx = clampl(da.dx, 100.0); da.dy = clampl(da.dy, 100.0); da.dz = clampl(da.dz, 100.0);
+            db.dx = clampl(db.dx, 100.0); db.dy = clampl(db.dy, 100.0); db.dz = clampl(db.dz, 100.0);
+            da.xx = clampl(da.xx, 1000.0); da.yy = clampl(da.yy, 1000.0); da.zz = clampl(da.zz, 1000.0);
+            db.xx = clampl(db.xx, 1000.0); db.yy = clampl(db.yy, 1000.0); db.zz = clampl(db.zz, 1000.0);
+            if (oka)
+                kra[f] = -uc.x * da.dx - vc.x * da.dy - wc.x * da.dz - gpa[f] / r2.x +
+                         nua * (da.xx + da.yy + da.zz) + sa[f];
+            if (okb)
+                krb[f] = -uc.y * db.dx - vc.y * db.dy - wc.y * db.dz - gpb[f] / r2.y +
+                         nub * (db.xx + db.yy + db.zz) + sb[f];
+            const double ta = (f == 0) ? da.dx : (f == 1 ? da.dy : da.dz);
+            const double tb = (f == 0) ? db.dx : (f == 1 ? db.dy : db.dz);
+            diva = (f == 0) ? ta : diva + ta;
+            divb = (f == 0) ? tb : divb + tb;
+        }
+        if (oka) kra[3] = -0.1 * r2.x * fmax(-10.0, fmin(10.0, diva));
+        if (okb) krb[3] = -0.1 * r2.y * fmax(-10.0, fmin(10.0, divb));
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
