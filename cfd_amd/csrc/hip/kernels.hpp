@@ -866,8 +866,11 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
         }
         __syncthreads();
     };
-    // block partial -> partials[slot][block] -> barrier -> grid total (thread 0)
-    auto gsum = [&](int slot, double v) __attribute__((always_inline)) {
+    // block partial -> partials[slot][block] -> barrier (gsum_begin); every
+    // workgroup then sums the partials in the same fixed tree (gsum_end,
+    // total in thread 0). The next phase's loads of each thread's first cell
+    // are issued between the two, so they overlap the partials' round trip.
+    auto gsum_begin = [&](int slot, double v) __attribute__((always_inline)) {
         v = wave_sum(v);
         if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
         __syncthreads();
@@ -878,8 +881,8 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
             store_sc1(&partials[slot * CGS_MAX_WG + blockIdx.x], b);
         }
         barrier();
-        // every workgroup: wave w sums partials [64 w, 64 w + 64), then the
-        // wave totals in order (the same fixed tree in every workgroup)
+    };
+    auto gsum_end = [&](int slot) __attribute__((always_inline)) {
         double t = (threadIdx.x < nb) ? load_sc1(&partials[slot * CGS_MAX_WG + threadIdx.x]) : 0.0;
         t = wave_sum(t);
         if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
@@ -889,7 +892,7 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
 #pragma unroll
             for (int w = 0; w < CGS_THREADS / 64; ++w) tot += sh[w];
         }
-        __syncthreads();  // sh is reused by the next gsum
+        __syncthreads();  // sh is reused by the next reduction
         return tot;
     };
     auto cell = [&](long long e) __attribute__((always_inline)) {
@@ -900,6 +903,52 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
         return k * g.ps + j * g.px + i;
     };
     const long long stride = (long long)nb * CGS_THREADS;
+    const long long e0 = (long long)blockIdx.x * CGS_THREADS + threadIdx.x;
+    const bool has0 = e0 < ncell;
+    const long long c0 = cell(has0 ? e0 : 0);  // a valid address either way
+    // the 7 stencil points of a cell: centre, x-, x+, y-, y+, z-, z+
+    auto pts = [&](long long c, long long (&q)[7]) __attribute__((always_inline)) {
+        q[0] = c; q[1] = c - 1; q[2] = c + 1; q[3] = c - g.px; q[4] = c + g.px;
+        q[5] = c - g.sz; q[6] = c + g.sz;
+    };
+    long long q0s[7];
+    pts(c0, q0s);
+    // phase A operands of cell c0: r and p_old at its stencil points
+    double ar[7], ap[7];
+    auto loadA = [&](const double* po_, bool first_) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            ar[t] = load_sc1(&r[q0s[t]]);
+            ap[t] = first_ ? 0.0 : load_sc1(&po_[q0s[t]]);
+        }
+    };
+    // phase A of one cell from its operands: p = r + beta p_old, A p
+    auto cellA = [&](long long c, const double (&rv)[7], const double (&pv)[7], bool first_,
+                     double beta, double* pn_, double& acc) __attribute__((always_inline)) {
+        double pp[7];
+#pragma unroll
+        for (int t = 0; t < 7; ++t) pp[t] = first_ ? rv[t] : rv[t] + beta * pv[t];
+        const double Ap = -lap7(L, pp[0], pp[1], pp[2], pp[3], pp[4], pp[5], pp[6]);
+        store_sc1(&pn_[c], pp[0]);
+        acc += pp[0] * Ap;
+    };
+    // phase B operands of cell c0: p_it at its stencil points, r, x
+    double bp[7], brr, bx;
+    auto loadB = [&](const double* pn_) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 7; ++t) bp[t] = load_sc1(&pn_[q0s[t]]);
+        brr = load_sc1(&r[c0]);
+        bx = x[c0];
+    };
+    auto cellB = [&](long long c, const double (&pv)[7], double rv, double xv, double al,
+                     double ma, double& acc) __attribute__((always_inline)) {
+        const double Ap = -lap7(L, pv[0], pv[1], pv[2], pv[3], pv[4], pv[5], pv[6]);
+        x[c] = xv + al * pv[0];
+        const double rn = rv + ma * Ap;
+        store_sc1(&r[c], rn);
+        acc += rn * rn;
+    };
+    loadA(pb, true);  // iteration 0: p = r
     for (int it = 0;; ++it) {
         if (ls.done) break;
         double* pn = (it & 1) ? pb : pa;
@@ -908,21 +957,23 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
         const double beta = first ? 0.0 : ls.beta;
         // phase A: p_it = r + beta p_{it-1} (formed at the neighbours too), (p, A p)
         double acc = 0.0;
-        for (long long e = (long long)blockIdx.x * CGS_THREADS + threadIdx.x; e < ncell;
-             e += stride) {
+        if (has0) cellA(c0, ar, ap, first, beta, pn, acc);
+        for (long long e = e0 + stride; e < ncell; e += stride) {
             const long long c = cell(e);
-            auto P = [&](long long q) __attribute__((always_inline)) {
-                const double rv = load_sc1(&r[q]);
-                return first ? rv : rv + beta * load_sc1(&po[q]);
-            };
-            const double pc = P(c);
-            const double Ap = -lap7(L, pc, P(c - 1), P(c + 1), P(c - g.px), P(c + g.px),
-                                    P(c - g.sz), P(c + g.sz));
-            store_sc1(&pn[c], pc);
-            acc += pc * Ap;
+            long long q[7];
+            pts(c, q);
+            double rv[7], pv[7];
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                rv[t] = load_sc1(&r[q[t]]);
+                pv[t] = first ? 0.0 : load_sc1(&po[q[t]]);
+            }
+            cellA(c, rv, pv, first, beta, pn, acc);
         }
-        const double tA = gsum(0, acc);
+        gsum_begin(0, acc);
         if (bad) break;
+        loadB(pn);
+        const double tA = gsum_end(0);
         if (threadIdx.x == 0) fin_A(&ls, tA, it);
         __syncthreads();
         if (ls.done) break;
@@ -930,20 +981,20 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
         const double al = ls.alpha[it % CG_XFOLD];
         const double ma = -al;
         acc = 0.0;
-        for (long long e = (long long)blockIdx.x * CGS_THREADS + threadIdx.x; e < ncell;
-             e += stride) {
+        if (has0) cellB(c0, bp, brr, bx, al, ma, acc);
+        for (long long e = e0 + stride; e < ncell; e += stride) {
             const long long c = cell(e);
-            const double pc = load_sc1(&pn[c]);
-            const double Ap = -lap7(L, pc, load_sc1(&pn[c - 1]), load_sc1(&pn[c + 1]),
-                                    load_sc1(&pn[c - g.px]), load_sc1(&pn[c + g.px]),
-                                    load_sc1(&pn[c - g.sz]), load_sc1(&pn[c + g.sz]));
-            x[c] = x[c] + al * pc;
-            const double rn = load_sc1(&r[c]) + ma * Ap;
-            store_sc1(&r[c], rn);
-            acc += rn * rn;
+            long long q[7];
+            pts(c, q);
+            double pv[7];
+#pragma unroll
+            for (int t = 0; t < 7; ++t) pv[t] = load_sc1(&pn[q[t]]);
+            cellB(c, pv, load_sc1(&r[c]), x[c], al, ma, acc);
         }
-        const double tB = gsum(1, acc);
+        gsum_begin(1, acc);
         if (bad) break;
+        loadA(pn, false);  // iteration it + 1: p_old = p_it
+        const double tB = gsum_end(1);
         if (threadIdx.x == 0) fin_B(&ls, tB, it);
         __syncthreads();
     }
