@@ -9,8 +9,8 @@ stderr so a long run is visibly alive).
              (tests/ghia.py) against the oracle's fixture
              tests/golden/cavity128_re1000_t50.json: the reference requires
              RMS < 0.10 (GHIA_RMS_TARGET_PROJECTION, test_cavity_backends.c:50)
-             and backends within 0.001 of each other (:43). Takes ~195 s on
-             one MI355X (1.9 ms per step with the persistent small-grid CG).
+             and backends within 0.001 of each other (:43). Takes ~150 s on
+             one MI355X (1.5 ms per step with the persistent small-grid CG).
   tg         configs[1]: Taylor-Green 3-D, nu = 0.01, dt = 1e-3, 100 steps,
              periodic BCs before every step (taylor_green_3d_reference.h:177-
              404); relative interior L2 of u, v against the reference's
