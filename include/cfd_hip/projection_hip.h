@@ -77,7 +77,7 @@ typedef struct {
                                      continues with the capped solve, as the reference GPU
                                      does (solver_projection_gpu.cu:717-733) */
     int relax_two_pass;           /* RB-SOR / Jacobi: 0 = device loop, RB-SOR in one pass per
-                                     iteration where possible (3-D, one device; default);
+                                     iteration in 3-D, on one device or on Z-slabs (default);
                                      1 = separate colour passes + residual pass with a host
                                      check per iteration (the r01 form); 2 = device loop with
                                      the two colour sweeps */
