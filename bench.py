@@ -16,6 +16,17 @@ split into N Z-slabs (hip_proj_create_slab), halo planes and CG dot products
 move over RCCL (a communicator our library creates from a unique id that
 rank 0 broadcasts over a gloo group), and the total work is fixed, so the
 scaling is strong.
+
+--case tg: configs[3], Taylor-Green at --size^3 on N Z-slabs.
+--case convection: configs[4], natural convection (Boussinesq energy
+equation coupled) on a --size x --size x --nz grid (default 1024 x 1024 x
+512), Red-Black SOR pressure solve, N Z-slabs over RCCL (the configuration
+BASELINE.json names on 8 GPUs); the setup restates
+tests/validation/test_natural_convection.c:140-293 (convection_setup). Its
+line reports MLUPS, RB-SOR iterations per step, per-rank relaxation timers
+(sweep / halo / all-reduce per iteration) and, at N = 1, a roofline on
+k_rb1 (24 B/cell per iteration). --dump PREFIX writes every rank's owned
+planes of u, v, w, p, T to PREFIX.rank<r>.npz (parity tests).
 """
 from __future__ import annotations
 
@@ -49,8 +60,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--size", type=int, default=512, help="grid points per axis")
-    ap.add_argument("--case", choices=("cavity", "tg"), default="cavity",
-                    help="cavity: configs[2] (default, every N); tg: configs[3] Taylor-Green")
+    ap.add_argument("--case", choices=("cavity", "tg", "convection"), default="cavity",
+                    help="cavity: configs[2] (default, every N); tg: configs[3] Taylor-Green; "
+                         "convection: configs[4] natural convection with RB-SOR")
+    ap.add_argument("--nz", type=int, default=0,
+                    help="convection: z points (default size / 2)")
+    ap.add_argument("--relax-max-iter", type=int, default=20000,
+                    help="convection: RB-SOR iteration cap per step (the 1024^2 x 512 solve "
+                         "needs ~13 000; the reference's default 5000 would fail the step)")
+    ap.add_argument("--dump", default="",
+                    help="convection: write each rank's owned planes to DUMP.rank<r>.npz")
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--dt", type=float, default=1e-4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,6 +123,18 @@ def main():
     torch.cuda.set_device(local)
 
     n = args.size
+    if args.case == "convection":
+        comm = None
+        if world > 1:
+            uid = [api.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = api.SlabComm.rccl(uid[0], rank, world, local)
+        run_convection(args, rank, world, local, comm, lib, torch, dist)
+        if comm is not None:
+            comm.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return
     tg = args.case == "tg"
     if tg:
         # configs[3]: Taylor-Green on [0, 2pi]^3, nu = 0.01, dt = 1e-3, periodic
@@ -350,6 +381,144 @@ def main():
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+# natural convection (test_natural_convection.c:50-61 constants)
+CONV_RA, CONV_PR, CONV_BETA, CONV_G = 1e3, 0.71, 0.003333, 9.81
+CONV_T_HOT, CONV_T_COLD, CONV_T_REF = 310.0, 290.0, 300.0
+BYTES_RB_ITER = 24.0  # k_rb1: read X, rhs; write Y
+
+
+def convection_setup(nx, ny, nz):
+    """configs[4]: the de Vahl Davis cavity of test_natural_convection.c:140-293
+    in 3-D on [0,1] x [0,1] x [0,0.5]: alpha, nu from Ra and Pr (:145-147), dt
+    half the thermal limit dx^2 / (2 alpha 3) (:150-154), hot x = 0 and cold
+    x = 1 Dirichlet walls, Neumann elsewhere, no-slip walls, fluid at rest
+    with T linear in x. Returns (grid, params, T0) with T0(x) the initial T
+    of every node of an x column."""
+    from cfd_amd import _abi as A
+    from cfd_amd import api
+    import numpy as np
+
+    dT = CONV_T_HOT - CONV_T_COLD
+    nu_alpha = CONV_G * CONV_BETA * dT / CONV_RA
+    alpha = math.sqrt(nu_alpha / CONV_PR)
+    nu = CONV_PR * alpha
+    g = api.Grid(nx, ny, nz, 0.0, 1.0, 0.0, 1.0, 0.0, 0.5)
+    dx = 1.0 / (nx - 1)
+    p = api.params_default()
+    p.dt = 0.5 * dx * dx / (2.0 * alpha * 3.0)
+    p.mu, p.alpha, p.beta, p.T_ref = nu, alpha, CONV_BETA, CONV_T_REF
+    p.gravity[0], p.gravity[1], p.gravity[2] = 0.0, -CONV_G, 0.0
+    p.source_amplitude_u = p.source_amplitude_v = 0.0
+    tb = p.thermal_bc
+    tb.left = tb.right = A.BC_TYPE_DIRICHLET
+    tb.top = tb.bottom = tb.front = tb.back = A.BC_TYPE_NEUMANN
+    tb.dirichlet_values.left, tb.dirichlet_values.right = CONV_T_HOT, CONV_T_COLD
+    T0 = CONV_T_HOT - dT * np.asarray(g.x)
+    return g, p, T0
+
+
+def run_convection(args, rank, world, local, comm, lib, torch, dist):
+    """configs[4] on N Z-slabs: projection_hip with the one-pass RB-SOR
+    pressure solve and the energy equation, fields resident in HBM."""
+    import numpy as np
+
+    from cfd_amd import _abi as A
+    from cfd_amd import _native, api
+
+    nx = ny = args.size
+    nz = args.nz or args.size // 2
+    g, p, T0 = convection_setup(nx, ny, nz)
+    ctx = api.HipProjection(nx, ny, nz, comm=comm, device=local,
+                            poisson_method=A.HIP_POISSON_REDBLACK,
+                            poisson_max_iter=args.relax_max_iter, relax_two_pass=0)
+    for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
+        ctx.fill(fid, 0.0)
+    ctx.set_field(A.HIP_FIELD_T, np.broadcast_to(T0[None, None, :], ctx.shape))
+    ctx.set_density(1.0)
+    for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W):
+        ctx.apply_dirichlet(fid, api.dirichlet())
+    ctx.synchronize()
+
+    def step():
+        s = ctx.step_device(g, p)
+        if s != A.CFD_SUCCESS:
+            raise RuntimeError(f"convection step failed {s}: {_native.last_error()}")
+        return ctx.poisson_stats().iterations
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = [step() for _ in range(args.steps)]
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ctx.enable_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+    kt = ctx.timing()
+    n_int = (nx - 2) * (ny - 2) * (nz - 2)
+    n_loc = (nx - 2) * (ny - 2) * (ctx.nz_local - 2)
+    tot_it = max(1, sum(iters))
+    per_it = lambda key: round(kt[key][0] / tot_it, 4) if kt[key][1] else None
+    mine = {"rank": rank, "planes": ctx.nz_local - 2,
+            "relax_sweep_ms_per_iter": per_it("relax"),
+            "relax_halo_ms_per_iter": per_it("halo"),
+            "relax_allreduce_ms_per_iter": per_it("allreduce"),
+            "timers_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
+    ranks = [mine]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    if args.dump:
+        loc, glob = ctx.owned()
+        out = {k: ctx.get_field(fid)[loc] for k, fid in
+               (("u", A.HIP_FIELD_U), ("v", A.HIP_FIELD_V), ("w", A.HIP_FIELD_W),
+                ("p", A.HIP_FIELD_P), ("T", A.HIP_FIELD_T))}
+        np.savez(f"{args.dump}.rank{rank}.npz", k0=glob.start, k1=glob.stop,
+                 iters=np.array(iters), **out)
+    roof = None
+    rms, rn = kt["relax"]
+    if world == 1 and rn:
+        # one k_rb1 launch per iteration on one device (the launches after
+        # convergence return at once and are not counted)
+        avg = rms / rn
+        ach = BYTES_RB_ITER * n_loc / (avg * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": "k_rb1<15, 64, true, false>",
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "algorithmic_bytes": BYTES_RB_ITER * n_loc, "bytes_per_cell": BYTES_RB_ITER,
+                "avg_launch_ms": round(avg, 4), "launches": rn}
+    ctx.close()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "MLUPS + achieved HBM GB/s, natural convection step (configs[4])",
+            "value": round(n_int * args.steps / elapsed / 1e6, 3),
+            "unit": "MLUPS", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (fluid at rest, T linear in x, generated in HBM)",
+            "config": {"workload": f"{nx}x{ny}x{nz} natural convection Ra=1e3, Pr=0.71, "
+                                   "projection_hip with the one-pass RB-SOR pressure solve",
+                       "grid": [nx, ny, nz], "interior_cells": n_int,
+                       "relax_max_iter": args.relax_max_iter,
+                       "parallelism": f"z-slab x{world} (RCCL halo)" if world > 1
+                                      else "single GPU"},
+            "rbsor_iters_per_step": iters,
+            "rbsor_iter_ms": round(elapsed * 1e3 / tot_it, 4),
+            "roofline": roof, "ranks": ranks, "cpu_baseline": None}))
 
 
 # timer -> kernel symbol in the PMC profile (the CG sweeps are named per variant)

@@ -576,14 +576,25 @@ class HipProjection:
         return self._lib().hip_proj_device_bytes(self._ctx)
 
     def poisson_solve(self, method: int, x: np.ndarray, rhs: np.ndarray, dx, dy, dz,
-                      params: Optional[A.PoissonParams] = None):
-        """hip_proj_poisson_solve: solves in place on x; returns (status, stats)."""
+                      params: Optional[A.PoissonParams] = None,
+                      bc_mode: int = A.HIP_POISSON_BC_NEUMANN,
+                      bc_values: Optional[np.ndarray] = None):
+        """hip_proj_poisson_solve (bc_mode NEUMANN) or hip_proj_poisson_solve_ex
+        (NONE / FIXED with bc_values): solves in place on x; returns (status, stats)."""
         assert x.dtype == np.float64 and x.flags["C_CONTIGUOUS"] and x.shape == self.shape
         r = np.ascontiguousarray(rhs, dtype=np.float64)
         st = A.PoissonStats()
-        s = self._lib().hip_proj_poisson_solve(
+        prm = C.byref(params) if params is not None else None
+        if bc_mode == A.HIP_POISSON_BC_NEUMANN and bc_values is None:
+            s = self._lib().hip_proj_poisson_solve(
+                self._ctx, method, x.ctypes.data_as(A.c_double_p),
+                r.ctypes.data_as(A.c_double_p), dx, dy, dz, prm, C.byref(st))
+            return s, st
+        bv = None if bc_values is None else np.ascontiguousarray(bc_values, dtype=np.float64)
+        s = self._lib().hip_proj_poisson_solve_ex(
             self._ctx, method, x.ctypes.data_as(A.c_double_p), r.ctypes.data_as(A.c_double_p),
-            dx, dy, dz, C.byref(params) if params is not None else None, C.byref(st))
+            dx, dy, dz, prm, C.byref(st), bc_mode,
+            bv.ctypes.data_as(A.c_double_p) if bv is not None else None)
         return s, st
 
     def cg_fixed_iters(self, rhs: np.ndarray, dx, dy, dz, iters: int) -> float:

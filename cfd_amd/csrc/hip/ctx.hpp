@@ -61,6 +61,11 @@ struct hip_proj_ctx {
     SGeo sgeo{};       // row-pair CG sweep tiling
     SGeo sg_edge{}, sg_int{};  // slabs: sweep B split into edge planes + interior
     SGeo rgeo{};               // single-pass RB-SOR tiling (k_rb1)
+    // slabs: one k_rb1 iteration as three launches sharing one reduction --
+    // interior part 1 (overlaps the R halo exchange), the two edge planes,
+    // interior part 2 (overlaps the exchange of the new iterate's edge planes)
+    SGeo rg_in1{}, rg_edge{}, rg_in2{};
+    int split_rb = 0;
     int rb1_tc = 64;           // k_rb1 tile width in x pairs (64, 32, 16)
     SGeo pgeo{};               // predictor / corrector z-march tiling (k_pred2, k_corr2)
     int split_b = 0;

@@ -60,9 +60,12 @@ struct Lap {
     double dx2_inv, dy2_inv, inv_dz2;  // linear_solver_cg.c:103-110
 };
 
-// x is updated every CG_XFOLD iterations: sweep B of iteration it with
-// it % CG_XFOLD == CG_XFOLD - 1 folds the CG_XFOLD pending alpha_j p_j into x;
+// x is updated every CG_XFOLD iterations: sweep A of iteration it with
+// it % CG_XFOLD == 0, it > 0, folds the CG_XFOLD pending alpha_j p_j
+// (j = it - 4 .. it - 1) into x before p_it overwrites slot it % CG_XFOLD;
 // the search directions live in a ring of CG_XFOLD buffers (p_j in [j % CG_XFOLD]).
+// A solve that stops after iteration it therefore leaves it % CG_XFOLD + 1
+// (1 .. CG_XFOLD) updates pending, in distinct ring slots, for k_cg_finalize.
 constexpr int CG_XFOLD = 4;
 
 // Device-resident CG state; written only by the finishing (last) workgroup.
@@ -402,6 +405,9 @@ struct SGeo {
     int kmode;
     int part_ofs, part_total;
     int kofs;  // global index of local plane 0 (Z-slabs; colour parity)
+    // kmode 2 (k_rb1 on slabs): tiles cover planes [kt0, kt1) only, while
+    // k0 / k1 still bound the planes that are updated
+    int kt0, kt1;
 };
 
 __device__ __forceinline__ int xcd_tile(int b, int nt) {
@@ -1009,11 +1015,13 @@ static __global__ __launch_bounds__(CGS_THREADS) void k_cg_small(Geo g, Lap L,
 }
 
 // Apply the x += alpha_j p_j the sweeps have not folded yet (j in [xdone,
-// nalpha), at most CG_XFOLD - 1 of them), in order, partial sums in a register
-// (bitwise the reference's sequential updates).
+// nalpha), at most CG_XFOLD of them: a stop after iteration it = 4m + 3
+// leaves alpha_{4m} .. alpha_{4m+3}, whose p_j still sit in the four ring
+// slots), in order, partial sums in a register (bitwise the reference's
+// sequential updates).
 static __global__ __launch_bounds__(NT) void k_cg_finalize(Geo g, PRing pr,
                                                     double* __restrict__ x, const CgState* st) {
-    const int j0 = st->xdone, j1 = st->nalpha;  // at most CG_XFOLD - 1 pending
+    const int j0 = st->xdone, j1 = st->nalpha;  // at most CG_XFOLD pending
     if (j0 >= j1) return;
     const int ntiles = g.tiles_x * g.tiles_y * g.tiles_z;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -2313,8 +2321,20 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
     const int rlo = max(r - 1, 0), rhi = min(r + 1, TR - 1);  // y neighbours' rows
     const int i0 = tx * OX - 2 + 2 * c;  // even; the pair is (i0, i0 + 1)
     const int j = ty * OY - 2 + r;       // grid row
-    const int kb = g.k0 + tz * g.kc;
-    const int ke = min(kb + g.kc, g.k1);
+    // kmode 1: the slab's two edge planes (tz 0 -> k0, tz 1 -> k1 - 1);
+    // kmode 2: the planes [kt0, kt1); else [k0, k1). A march over a plane
+    // range still forms R on its two lower neighbour planes (prologue), so
+    // the ranges of one iteration's launches give the one-launch Y.
+    int kb, ke;
+    if (g.kmode == 1) {
+        kb = (tz == 0) ? g.k0 : g.k1 - 1;
+        ke = kb + 1;
+    } else {
+        const int kt0 = (g.kmode == 2) ? g.kt0 : g.k0;
+        const int kt1 = (g.kmode == 2) ? g.kt1 : g.k1;
+        kb = kt0 + tz * g.kc;
+        ke = min(kb + g.kc, kt1);
+    }
     const bool xin = (i0 >= 0 && i0 < g.nx);
     const bool ld = xin && j >= 0 && j < g.ny;
     const bool jin = (j >= 1 && j <= g.ny - 2);
@@ -2479,19 +2499,24 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
     if (lane == 0) sh[w] = m;
     __syncthreads();
     double* shs = &xb[0][0][0][0];
+    // an iteration split over several launches (slabs: kmode 1 / 2) shares
+    // one partials array: this launch owns [part_ofs, part_ofs + gridDim.x)
+    // of part_total, and the last of all part_total workgroups (the last
+    // launch on the stream) finishes the max
+    const unsigned ptot = g.part_total ? (unsigned)g.part_total : gridDim.x;
     if (threadIdx.x == 0) {
         double a = 0.0;
         for (int v = 0; v < NW; ++v) a = fmax(a, sh[v]);
-        store_sc1(&partials[blockIdx.x], a);
+        store_sc1(&partials[g.part_ofs + blockIdx.x], a);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned tk = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
-        flag = (tk == gridDim.x - 1) ? 1 : 0;
+        flag = (tk == ptot - 1) ? 1 : 0;
     }
     __syncthreads();
     if (flag == 0) return;
     double a = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += 1024) a = fmax(a, load_sc1(&partials[b]));
+    for (unsigned b = threadIdx.x; b < ptot; b += 1024) a = fmax(a, load_sc1(&partials[b]));
     a = wave_max(a);
     if (lane == 0) shs[w] = a;
     __syncthreads();

@@ -477,15 +477,53 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             timed(c, HIP_KT_RELAX, [&] {
                 hipExtLaunchKernelGGL(k_rb_edge_r, dim3(ne), dim3(256), 0, c->stream, c->ta,
                                       c->tb, 0, c->rgeo, rc, xi, c->rhs, RH);
-            });
-            ST_TRY(halo(c, {RH}));
-            timed(c, HIP_KT_RELAX, [&] {
-                hipExtLaunchKernelGGL((k_rb1<FL, 64, true, true>), dim3(nb1), dim3(1024), 0,
-                                      c->stream, c->ta, c->tb, 0, c->rgeo, rc, xi, xo, c->rhs,
-                                      c->rxst, c->partials, c->counter, it, (const double*)RH,
-                                      c->geo.lo_face ? 0 : 1, c->geo.hi_face ? 0 : 1, mb, dred);
-            });
-            ST_TRY(finish(it));
+            }, it);
+            auto rb1 = [&](const SGeo& sg) {
+                const unsigned nbx = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
+                timed(c, HIP_KT_RELAX, [&] {
+                    hipExtLaunchKernelGGL((k_rb1<FL, 64, true, true>), dim3(nbx), dim3(1024), 0,
+                                          c->stream, c->ta, c->tb, 0, sg, rc, xi, xo, c->rhs,
+                                          c->rxst, c->partials, c->counter, it, (const double*)RH,
+                                          c->geo.lo_face ? 0 : 1, c->geo.hi_face ? 0 : 1, mb,
+                                          dred);
+                }, it);
+            };
+            // exchange of `f`'s edge planes on the side stream (halo
+            // communicator), ordered after the main stream's work so far
+            auto side_halo = [&](double* f) -> cfd_status_t {
+                HIP_TRY(hipEventRecord(c->ev_b, c->stream));
+                HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
+                double* ff[1] = {f};
+                ST_TRY(timed_span(c, c->hstream, HIP_KT_HALO, [&] {
+                    return c->comm->halo(c->hstream, ff, 1, c->ps, (int)c->nz, false);
+                }, it));
+                HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
+                return CFD_SUCCESS;
+            };
+            if (c->split_rb) {
+                // R's edge planes travel while interior part 1 (which needs no
+                // halo R) runs; the edge planes of Y follow, and their exchange
+                // overlaps interior part 2 and the residual's all-reduce. The
+                // three launches write disjoint planes of Y and share one
+                // L-inf reduction, so Y and the decision are the one-launch ones.
+                ST_TRY(side_halo(RH));
+                rb1(c->rg_in1);
+                HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
+                rb1(c->rg_edge);
+                ST_TRY(side_halo(xo));
+                rb1(c->rg_in2);
+                if (!mb)
+                    ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] { return finish(it); },
+                                      it));
+                HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
+            } else {
+                ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {RH}); }, it));
+                rb1(c->rgeo);
+                if (!mb)
+                    ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] { return finish(it); },
+                                      it));
+                ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {xo}); }, it));
+            }
         } else if (single) {
             // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the
             // end-of-step loads (experiments)
@@ -514,7 +552,8 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             sweep(RX_JACOBI, xi, xo, it);
             ST_TRY(finish(it));
         }
-        ST_TRY(halo(c, {xo}));
+        if (!(single && D))
+            ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {xo}); }, it));
         // the iteration's apply_bc: Neumann (linear_solver_redblack.c:139,
         // linear_solver_jacobi.c:118), or the caller's fixed boundary values,
         // or x's own boundary kept
@@ -582,6 +621,16 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
         return relax_solve_fused(c, method, rc, rel_tol, abs_tol, max_iter, check_interval);
     ResCoef res_c{rc.dx2, rc.dy2, rc.inv_dz2};
     const DirVals dv{};
+    // caller boundary modes (hip_proj_poisson_solve_ex): the iteration's
+    // apply_bc copies the shell from bcfix (FIXED) or keeps x's own (NONE);
+    // k_rx_shell does the copy, gated on an RxState that k_rx_init leaves
+    // undecided
+    const bool neumann_bc = c->poisson_bc == HIP_POISSON_BC_NEUMANN;
+    if (!neumann_bc) {
+        if (!c->rxst) HIP_TRY(hipMalloc((void**)&c->rxst, sizeof(RxState)));
+        hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
+                              c->rxst, rel_tol, abs_tol, max_iter, check_interval);
+    }
     ST_TRY(halo(c, {c->pn}));
     double res0 = 0.0;
     cfd_status_t s = residual_linf(c, c->pn, res_c, &res0);
@@ -615,11 +664,21 @@ static cfd_status_t relax_solve(hip_proj_ctx* c, int method, double dx, double d
                                    c->xt, c->rhs);
             });
             // memcpy(x, x_temp) + BC == swap buffers then BC (all boundary
-            // cells are rewritten by the Neumann gather)
+            // cells are rewritten by the Neumann gather; with a caller mode
+            // the shell is copied below)
             std::swap(c->pn, c->xt);
         }
         ST_TRY(halo(c, {c->pn}));
-        launch_bc(c, c->pn, 0, dv);
+        if (neumann_bc) {
+            launch_bc(c, c->pn, 0, dv);
+        } else if (c->poisson_bc == HIP_POISSON_BC_FIXED || method != HIP_POISSON_REDBLACK) {
+            // FIXED: the caller's values; NONE + Jacobi: the iterate's previous
+            // boundary (now in xt), as the fused loop keeps it. NONE + RB-SOR
+            // updates in place and never writes the shell.
+            const double* src = (c->poisson_bc == HIP_POISSON_BC_FIXED) ? c->bcfix : c->xt;
+            hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream,
+                                  c->ta, c->tb, 0, c->geo, c->rxst, src, c->pn, 0);
+        }
         if (iter % check_interval == 0) {
             s = residual_linf(c, c->pn, res_c, &res);
             if (s != CFD_SUCCESS) return s;
@@ -875,6 +934,36 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         rg.kc = std::max(1, std::min(rg.kc, nint_k));
         rg.tiles_z = (nint_k + rg.kc - 1) / rg.kc;
         n_partials = std::max(n_partials, rg.tiles_x * rg.tiles_y * rg.tiles_z);
+        // Z-slabs: output planes k0+1 .. k1-2 split into two halves around
+        // the edge planes (relax_solve_fused); CFD_HIP_RB_SPLIT=0 keeps the
+        // one-launch iteration with blocking exchanges (A/B)
+        const char* es = getenv("CFD_HIP_RB_SPLIT");
+        c->split_rb = (c->nranks > 1 && nint_k >= 4 && !(es && atoi(es) == 0)) ? 1 : 0;
+        if (c->split_rb) {
+            const int a0 = g.k0 + 1, a1 = g.k1 - 1;  // interior output planes [a0, a1)
+            const int mid = a0 + (a1 - a0) / 2;
+            auto range = [&](SGeo& q, int lo, int hi) {
+                q = rg;
+                q.kmode = 2;
+                q.kt0 = lo;
+                q.kt1 = hi;
+                q.kc = std::max(1, std::min(rg.kc, hi - lo));
+                q.tiles_z = (hi - lo + q.kc - 1) / q.kc;
+            };
+            range(c->rg_in1, a0, mid);
+            range(c->rg_in2, mid, a1);
+            c->rg_edge = rg;
+            c->rg_edge.kmode = 1;
+            c->rg_edge.kc = 1;
+            c->rg_edge.tiles_z = 2;
+            const int xy = rg.tiles_x * rg.tiles_y;
+            const int n1 = xy * c->rg_in1.tiles_z, ne = xy * 2, n2 = xy * c->rg_in2.tiles_z;
+            c->rg_in1.part_ofs = 0;
+            c->rg_edge.part_ofs = n1;
+            c->rg_in2.part_ofs = n1 + ne;
+            c->rg_in1.part_total = c->rg_edge.part_total = c->rg_in2.part_total = n1 + ne + n2;
+            n_partials = std::max(n_partials, n1 + ne + n2);
+        }
     }
     {   // predictor / corrector: 128 x PR_TY x kc tiles, >= ~8 workgroups per CU
         SGeo& pg = c->pgeo;
@@ -922,6 +1011,8 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     HIP_TRY(hipMalloc((void**)&c->st, sizeof(CgState)));
     HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
     // x2: the single-reduction CG reduces two values per workgroup
+    // k_cg_small indexes its two partial slots by CGS_MAX_WG whatever the CU count
+    n_partials = std::max(n_partials, CGS_MAX_WG);
     HIP_TRY(hipMalloc((void**)&c->partials, 2 * sizeof(double) * n_partials));
     HIP_TRY(hipMalloc((void**)&c->counter, 64));
     HIP_TRY(hipMemsetAsync(c->counter, 0, 64, c->stream));

@@ -33,6 +33,7 @@ static int g_have_pparams = 0;
 static int g_gpu_rhs = 0;     /* 1: rhs = div / dt, the reference GPU's (solver_projection_gpu.cu:706-707) */
 static poisson_solver_params_t g_pparams;
 static double g_phase_ms[4];
+static poisson_solver_stats_t g_last_pst; /* the last projection step's Poisson stats */
 
 void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 void oracle_set_poisson_cap(int n) { g_poisson_cap = n < 0 ? 0 : n; }
@@ -43,6 +44,7 @@ void oracle_set_projection_poisson_params(const poisson_solver_params_t* p) {
 void oracle_set_gpu_rhs(int on) { g_gpu_rhs = on ? 1 : 0; }
 int oracle_get_threads(void) { return g_threads; }
 void oracle_last_phase_ms(double out[4]) { memcpy(out, g_phase_ms, sizeof(g_phase_ms)); }
+void oracle_last_poisson_stats(poisson_solver_stats_t* out) { if (out) *out = g_last_pst; }
 
 static double now_ms(void) {
     struct timeval tv;
@@ -53,6 +55,8 @@ static double now_ms(void) {
 #define DO_PRAGMA(x) _Pragma(#x)
 #define PAR DO_PRAGMA(omp parallel for collapse(2) schedule(static) if(g_threads > 1) num_threads(g_threads))
 #define PAR_SUM(v) DO_PRAGMA(omp parallel for collapse(2) schedule(static) reduction(+:v) if(g_threads > 1) num_threads(g_threads))
+/* L-inf is a max, so a parallel reduction is bitwise the sequential one */
+#define PAR_MAX(v) DO_PRAGMA(omp parallel for collapse(2) schedule(static) reduction(max:v) if(g_threads > 1) num_threads(g_threads))
 
 /* ------------------------------------------------------------------------ */
 /* grid / field / params (grid.c:9-127, solver_explicit_euler.c:58-122)     */
@@ -495,6 +499,7 @@ double oracle_poisson_residual_linf(const double* x, const double* rhs, size_t n
     double inv_dz2 = (dz > 0.0) ? (1.0 / (dz * dz)) : 0.0;
     size_t sz = (nz > 1) ? nx * ny : 0, k0 = (nz > 1) ? 1 : 0, k1 = (nz > 1) ? nz - 1 : 1;
     double mx = 0.0;
+    PAR_MAX(mx)
     for (size_t k = k0; k < k1; k++)
         for (size_t j = 1; j < ny - 1; j++)
             for (size_t i = 1; i < nx - 1; i++) {
@@ -593,6 +598,9 @@ static void redblack_sweep(void* vctx, double* x, double* xt, const double* rhs)
     relax_ctx* c = (relax_ctx*)vctx;
     size_t nx = c->nx, ny = c->ny, sz = c->sz;
     for (int pass = 0; pass < 2; pass++) {
+        /* one colour's cells read only the other colour: any order within a
+         * pass is bitwise the reference's loop */
+        PAR
         for (size_t k = c->k0; k < c->k1; k++)
             for (size_t j = 1; j < ny - 1; j++) {
                 size_t i0 = ((j + k) % 2 == 0) ? (pass == 0 ? 1 : 2) : (pass == 0 ? 2 : 1);
@@ -953,6 +961,7 @@ cfd_status_t oracle_projection_step(flow_field* field, const grid* grid,
         ps = oracle_cg_solve(pn, rhs, nx, ny, nz, dx, dy, dz, pp, &pst);
     if (g_poisson_cap > 0) { ps = CFD_SUCCESS; pst.status = POISSON_CONVERGED; }
     if (poisson_iters) *poisson_iters = pst.iterations;
+    g_last_pst = pst;
     double t3 = now_ms();
     /* poisson_solve_3d returns -1 unless converged (linear_solver.c:691-704) */
     if (!(ps == CFD_SUCCESS && pst.status == POISSON_CONVERGED)) { st = CFD_ERROR_MAX_ITER; goto done; }

@@ -107,6 +107,9 @@ cfd_status_t oracle_projection_step(flow_field* field, const grid* g,
 /* Phase timings (ms) of the most recent oracle_projection_step, for the CPU
  * baseline: [0] predictor, [1] divergence, [2] poisson, [3] corrector+rest. */
 void oracle_last_phase_ms(double out[4]);
+/* Poisson stats (iterations, initial / final residual, status) of the last
+ * oracle_projection_step. */
+void oracle_last_poisson_stats(poisson_solver_stats_t* out);
 
 /* CG with a fixed iteration count and no early exit (baseline microbench,
  * SURVEY.md §8d). Returns wall ms. */

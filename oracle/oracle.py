@@ -54,6 +54,7 @@ def lib():
         sig("oracle_projection_step", C.c_int, P(A.FlowField), P(A.Grid), P(A.SolverParams),
             P(A.SolverStats), C.c_int, P(C.c_int))
         sig("oracle_last_phase_ms", None, d)
+        sig("oracle_last_poisson_stats", None, P(A.PoissonStats))
         sig("oracle_cg_solve", C.c_int, d, d, sz, sz, sz, C.c_double, C.c_double, C.c_double,
             P(A.PoissonParams), P(A.PoissonStats))
         sig("oracle_redblack_solve", C.c_int, d, d, sz, sz, sz, C.c_double, C.c_double,
@@ -101,6 +102,13 @@ def projection_step(field, grid, params, poisson=A.ORACLE_POISSON_CG):
     s = lib().oracle_projection_step(field.ptr, grid.ptr, C.byref(params), C.byref(st),
                                      poisson, C.byref(it))
     return s, st, it.value
+
+
+def last_poisson_stats() -> A.PoissonStats:
+    """Poisson stats of the last projection_step (iterations, residuals, status)."""
+    st = A.PoissonStats()
+    lib().oracle_last_poisson_stats(C.byref(st))
+    return st
 
 
 def set_projection_poisson_params(params=None):

@@ -125,10 +125,108 @@ def cavity128_re1000(steps=100000, snap=1000):
                         iters=np.array(its, dtype=np.int32), **fields(f))
 
 
+CAV512_SNAP_STEPS = (1, 6, 25)
+CAV512_PLANES = (1, 255, 510)
+CAV512_ROWS = (1, 255, 509, 510)
+CAV512_COLS = (1, 255, 510)
+
+
+def plane_samples(a2: np.ndarray) -> dict:
+    """What the 512^3 fixture keeps of one z plane: a stride-4 lattice (plus
+    the last index), full rows j = 1, 255, 509, 510 (the lid's boundary layer
+    sits at j = 510), full columns i = 1, 255, 510, and sum / L2 / max |.|
+    of the whole plane."""
+    n = a2.shape[0]
+    idx = np.r_[np.arange(0, n, 4), n - 1] if (n - 1) % 4 else np.arange(0, n, 4)
+    rows = [j for j in CAV512_ROWS if j < n]
+    cols = [i for i in CAV512_COLS if i < a2.shape[1]]
+    return {"lattice_idx": idx, "lattice": a2[np.ix_(idx, idx)].copy(),
+            "rows_j": np.array(rows), "rows": a2[rows, :].copy(),
+            "cols_i": np.array(cols), "cols": a2[:, cols].T.copy(),
+            "stats": np.array([float(np.sum(a2)), float(np.sqrt(np.sum(a2 * a2))),
+                               float(np.max(np.abs(a2)))])}
+
+
+def field_norms(f) -> dict:
+    """L2 (sqrt of the pairwise sum of squares) and max |.| of the interior
+    of each field (the cells the step computes; the boundary u = 1 lid would
+    dominate a whole-field norm)."""
+    out = {}
+    for k in ("u", "v", "w", "p"):
+        a = np.ascontiguousarray(getattr(f, k)[1:-1, 1:-1, 1:-1])
+        out[k] = [float(np.sqrt(np.sum(a * a))), float(np.max(np.abs(a)))]
+    return out
+
+
+def cavity512_re1000(n=512, steps=25, state_dir="/tmp/cav512_state", threads=8):
+    """BASELINE configs[2] at its own size, on the bench's exact trajectory:
+    n^3 lid-driven cavity, Re = 1000, dt = 1e-4, from rest, lid u = 1 on
+    y = 1 and Neumann p before every step (bench.py make_ctx; the step keeps
+    the boundary faces, so applying them before every step is the same as
+    once), the reference's CG settings (rel 1e-6, abs 1e-10, 5000).
+    The oracle runs its OpenMP twin (the reference's projection_omp /
+    cg_omp_solve order of dot-product partials, solver_projection_omp.c:26-279)
+    on `threads` cores: about 5 min per step here, so the state is saved to
+    `state_dir` after every step and a rerun resumes.
+    Writes cavity{n}_re1000_steps.json (per step: CG iterations, initial /
+    final residual, L2 and max |.| of u, v, w, p) and, after the steps in
+    CAV512_SNAP_STEPS, cavity{n}_re1000_step{s}_planes.npz (plane_samples of
+    u, v, w, p at k in CAV512_PLANES)."""
+    import json
+    import time
+
+    sd = Path(state_dir)
+    sd.mkdir(parents=True, exist_ok=True)
+    oracle.set_threads(threads)
+    g, f, p = cases.cavity(n, n, n, Re=1000.0, dt=1e-4)
+    out_json = HERE / f"cavity{n}_re1000_steps.json"
+    rec = {"grid": [n, n, n], "re": 1000.0, "dt": 1e-4, "steps": [],
+           "oracle": f"oracle_projection_step, CG, OpenMP {threads} threads",
+           "generator": "tests/golden/make_golden.py cavity512"}
+    prog = sd / "progress.json"
+    if prog.exists():
+        rec = json.loads(prog.read_text())
+        for k in ("u", "v", "w", "p"):
+            getattr(f, k)[...] = np.load(sd / f"{k}.npy")
+        print(f"resumed after step {len(rec['steps'])}", flush=True)
+    while len(rec["steps"]) < steps:
+        s = len(rec["steps"]) + 1
+        t0 = time.time()
+        api.cavity_bc(f, 1.0)
+        st, sts, it = oracle.projection_step(f, g, p)
+        assert st == A.CFD_SUCCESS, st
+        ps = oracle.last_poisson_stats()
+        row = {"step": s, "cg_iters": it, "initial_residual": ps.initial_residual,
+               "final_residual": ps.final_residual, "max_velocity": sts.max_velocity,
+               "max_pressure": sts.max_pressure, "norms": field_norms(f),
+               "seconds": round(time.time() - t0, 1)}
+        rec["steps"].append(row)
+        print(json.dumps(row), flush=True)
+        if s in CAV512_SNAP_STEPS:
+            planes = {}
+            for k in ("u", "v", "w", "p"):
+                for kz in CAV512_PLANES:
+                    if kz < n:
+                        for key, val in plane_samples(getattr(f, k)[kz]).items():
+                            planes[f"{k}_k{kz}_{key}"] = val
+            np.savez_compressed(HERE / f"cavity{n}_re1000_step{s}_planes.npz", **planes)
+        out_json.write_text(json.dumps(rec, indent=1) + "\n")
+        if s < steps:
+            for k in ("u", "v", "w", "p"):
+                np.save(sd / f"{k}.npy", getattr(f, k))
+            prog.write_text(json.dumps(rec))
+
+
 if __name__ == "__main__":
     oracle.set_threads(1)
     if sys.argv[1:] == ["cavity128"]:
         cavity128_re1000()
+        sys.exit(0)
+    if sys.argv[1:2] == ["cavity512"]:
+        # optional: size steps state_dir (defaults: the bench's 512^3, 25 steps)
+        a = sys.argv[2:]
+        cavity512_re1000(int(a[0]) if a else 512, int(a[1]) if len(a) > 1 else 25,
+                         a[2] if len(a) > 2 else "/tmp/cav512_state")
         sys.exit(0)
     dvd_ra1e3()
     kat()

@@ -77,3 +77,74 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
     # the other CG variant measured beside the timed region
     cmp = d["cg_variant_compare"]
     assert cmp["cg_variant"] == 1 and cmp["cg_iters"] > 0 and cmp["ms_per_cg_iter_wall"] > 0
+
+
+def _oracle_convection(nx, ny, nz, steps):
+    """The oracle's run of bench.convection_setup: RB-SOR projection steps
+    with the energy equation (solver_projection.c:46-297 with the RB-SOR
+    solve, energy_solver.c:21-334)."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from cfd_amd import _abi as A
+    from cfd_amd import api
+    from oracle import oracle
+
+    g, p, T0 = bench.convection_setup(nx, ny, nz)
+    f = api.FlowField(nx, ny, nz)
+    f.u[...] = f.v[...] = f.w[...] = f.p[...] = 0.0
+    f.rho[...] = 1.0
+    f.T[...] = np.broadcast_to(T0[None, None, :], f.T.shape)
+    oracle.set_projection_poisson_params(oracle.poisson_params(max_iterations=20000))
+    its = []
+    try:
+        for _ in range(steps):
+            s, _, it = oracle.projection_step(f, g, p, A.ORACLE_POISSON_REDBLACK)
+            assert s == A.CFD_SUCCESS
+            its.append(it)
+    finally:
+        oracle.set_projection_poisson_params(None)
+    return f, its
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_convection_launcher_bitwise(hip_lib, tmp_path, world):
+    """configs[4]'s launcher (bench.py --case convection): 1 rank, and 2 ranks
+    over RCCL (shared device), at 24 x 20 x 18; every rank's owned planes
+    of u, v, w, p, T and the RB-SOR iteration counts bitwise the oracle's."""
+    import numpy as np
+
+    nx, nz, steps = 24, 18, 2
+    dump = tmp_path / "conv"
+    args = ["bench.py", "--gpus", str(world), "--case", "convection", "--size", str(nx),
+            "--nz", str(nz), "--steps", str(steps), "--warmup", "0", "--dump", str(dump)]
+    env = _env()
+    if world > 1:
+        env["CFD_BENCH_SHARED_GPU"] = "1"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={world}", "--rdzv-backend=c10d",
+               "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1"] + args
+    else:
+        cmd = [sys.executable] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d) and d["n_gpus"] == world and d["value"] > 0
+    assert len(d["ranks"]) == world
+    for q in d["ranks"]:
+        assert q["relax_sweep_ms_per_iter"] > 0
+        if world > 1:
+            assert q["relax_halo_ms_per_iter"] > 0
+    if world == 1:
+        assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["kernel"].startswith("k_rb1<")
+    fo, its = _oracle_convection(nx, nx, nz, steps)
+    assert d["rbsor_iters_per_step"] == its
+    got = {k: np.full((nz, nx, nx), np.nan) for k in ("u", "v", "w", "p", "T")}
+    for rk in range(world):
+        z = np.load(f"{dump}.rank{rk}.npz")
+        assert list(z["iters"]) == its
+        for k in got:
+            got[k][int(z["k0"]):int(z["k1"])] = z[k]
+    for k, a in got.items():
+        np.testing.assert_array_equal(a, getattr(fo, k), err_msg=k)

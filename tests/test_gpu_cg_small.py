@@ -93,3 +93,63 @@ def test_cg_small_cavity_steps_vs_oracle(hip_lib, monkeypatch):
         ref = getattr(fo, k)
         scale = max(1.0, float(np.max(np.abs(ref))))
         assert float(np.max(np.abs(getattr(fh, k) - ref))) / scale <= 1e-10, k
+
+
+def _fold_problem():
+    nx, ny, nz = 40, 30, 20
+    rng = np.random.default_rng(4)
+    rhs = np.zeros((nz, ny, nx))
+    rhs[1:-1, 1:-1, 1:-1] = rng.standard_normal((nz - 2, ny - 2, nx - 2))
+    return (nx, ny, nz), rhs, (1.0 / (nx - 1), 1.0 / (ny - 1), 1.0 / (nz - 1))
+
+
+def _match_oracle_x(x, prm, rhs, d):
+    xo = np.zeros_like(rhs)
+    so, sto = oracle.cg_solve(xo, rhs, *d, prm)
+    assert np.max(np.abs(x - xo)) / np.max(np.abs(xo)) < 1e-10
+    return so, sto
+
+
+@pytest.mark.parametrize("max_iter", [1, 3, 4, 5, 7, 8, 9, 12])
+def test_sweep_cg_fold_boundaries_capped(hip_lib, monkeypatch, max_iter):
+    """The sweep path folds x += alpha p every fourth iteration (in sweep A of
+    it = 4m) and k_cg_finalize applies what is pending when the loop stops:
+    1..4 updates depending on max_iter mod 4. A capped solve at every
+    residue class against the oracle's sequential updates
+    (linear_solver_cg.c:379-380,437-459): same status and count, x 1e-10."""
+    shape, rhs, d = _fold_problem()
+    prm = oracle.poisson_params(max_iterations=max_iter)
+    s, st, x, kt = _solve(shape, rhs, d, False, monkeypatch, prm)
+    assert kt["cg_small"][1] == 0
+    so, sto = _match_oracle_x(x, prm, rhs, d)
+    assert s == so == A.CFD_ERROR_MAX_ITER
+    assert st.iterations == sto.iterations == max_iter
+    assert st.final_residual == pytest.approx(sto.final_residual, rel=1e-9)
+
+
+@pytest.mark.parametrize("residue", [0, 1, 2, 3])
+def test_sweep_cg_fold_boundaries_converged(hip_lib, monkeypatch, residue):
+    """Convergence (not a cap) after a chosen iteration count in each residue
+    class mod 4: the relative tolerance is placed between the oracle's
+    residual after m iterations, a new minimum, and the smallest one before
+    it, so both solvers stop at m."""
+    shape, rhs, d = _fold_problem()
+    res = {}
+    for m in range(1, 40):
+        xo = np.zeros_like(rhs)
+        _, sto = oracle.cg_solve(xo, rhs, *d, oracle.poisson_params(max_iterations=m))
+        res[m] = sto.final_residual
+        res0 = sto.initial_residual
+    pick = None
+    for m in range(8, 40):
+        prev = min(res[q] for q in range(1, m))
+        if m % 4 == residue and res[m] < prev / 1.05:
+            pick = (m, float(np.sqrt(res[m] * prev)) / res0)
+            break
+    assert pick is not None, res
+    m, rel = pick
+    prm = oracle.poisson_params(tolerance=rel, absolute_tolerance=0.0, max_iterations=1000)
+    s, st, x, _ = _solve(shape, rhs, d, False, monkeypatch, prm)
+    so, sto = _match_oracle_x(x, prm, rhs, d)
+    assert s == so == A.CFD_SUCCESS
+    assert st.iterations == sto.iterations == m

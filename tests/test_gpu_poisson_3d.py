@@ -26,7 +26,7 @@ import numpy as np
 import pytest
 
 from cfd_amd import _abi as A
-from cfd_amd import _native
+from cfd_amd import _native, api
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -290,3 +290,41 @@ def test_jacobi_requires_temp_buffer(hip_lib):
     pb = Problem(9, 9)
     rc, _, _ = gpu_solve(A.POISSON_METHOD_JACOBI, pb, pb.dirichlet, with_xt=False)
     assert rc == A.CFD_ERROR_INVALID
+
+
+HIP_METHOD = {A.POISSON_METHOD_JACOBI: A.HIP_POISSON_JACOBI,
+              A.POISSON_METHOD_REDBLACK_SOR: A.HIP_POISSON_REDBLACK}
+
+
+@pytest.mark.parametrize("sweep_rows", [4, 16])
+@pytest.mark.parametrize("method", [A.POISSON_METHOD_JACOBI, A.POISSON_METHOD_REDBLACK_SOR])
+@pytest.mark.parametrize("which", ["dirichlet", "keep"])
+def test_caller_bc_modes_every_relaxation_path(hip_lib, sweep_rows, method, which):
+    """hip_proj_poisson_solve_ex's caller boundary modes (FIXED values, NONE =
+    keep x's boundary) on both relaxation drivers: the device loop (16-row
+    sweep tiles) and the per-iteration host loop (4-row tiles, k_rb_pass /
+    k_jacobi), bitwise the oracle running the same override as its apply_bc.
+    The context starts Jacobi's x_temp as a copy of x, so the oracle gets
+    x_temp = x0 (the reference copies x_temp's boundary into x)."""
+    pb = Problem(13, 11)
+    if which == "dirichlet":
+        x0 = np.zeros(pb.shape)
+        pb.dirichlet(x0)
+        bc, mode, vals = pb.dirichlet, A.HIP_POISSON_BC_FIXED, pb.exact
+    else:
+        x0, _ = _random_start(pb, 11)
+        bc, mode, vals = pb.keep, A.HIP_POISSON_BC_NONE, None
+    ctx = api.HipProjection(pb.nx, pb.ny, pb.nz, sweep_rows=sweep_rows)
+    try:
+        x = x0.copy()
+        rc, st = ctx.poisson_solve(HIP_METHOD[method], x, pb.rhs, pb.dx, pb.dy, pb.dz,
+                                   _params(method), bc_mode=mode, bc_values=vals)
+    finally:
+        ctx.close()
+    assert rc in (A.CFD_SUCCESS, A.CFD_ERROR_MAX_ITER), _native.last_error()
+    want = oracle_solve(method, pb, bc, x0=x0, xt0=x0.copy())
+    _match_oracle(method, (rc, st, x), want)
+    if which == "dirichlet":
+        b = np.ones(pb.shape, bool)
+        b[1:-1, 1:-1, 1:-1] = False
+        np.testing.assert_array_equal(x[b], pb.exact[b])

@@ -235,14 +235,21 @@ def test_slab_poisson_cg_vs_oracle(hip_lib):
 
 
 @pytest.mark.parametrize("method", [A.HIP_POISSON_REDBLACK, A.HIP_POISSON_JACOBI])
-@pytest.mark.parametrize("nranks,two_pass,maxit", [(4, 0, None), (4, 1, None), (4, 2, None),
-                                                   (2, 0, None), (3, 0, 11)])
-def test_slab_poisson_relax_bitwise(hip_lib, method, nranks, two_pass, maxit):
+@pytest.mark.parametrize("nranks,two_pass,maxit,split", [
+    (4, 0, None, "1"), (4, 1, None, "1"), (4, 2, None, "1"), (2, 0, None, "1"),
+    (3, 0, 11, "1"), (2, 0, None, "0"), (3, 0, 11, "0")])
+def test_slab_poisson_relax_bitwise(hip_lib, monkeypatch, method, nranks, two_pass, maxit,
+                                    split):
     """Slab RB-SOR / Jacobi, fused device loop (residual max across ranks) and
     two-pass form: bitwise the oracle, iteration counts and status included;
     every rank's halo planes end equal to the neighbours' owned planes.
     RB-SOR: relax_two_pass 0 = one pass per iteration (k_rb_edge_r, R halo,
-    k_rb1<DIST>), 2 = the two colour sweeps of k_rx, 1 = the unfused form."""
+    k_rb1<DIST>), 2 = the two colour sweeps of k_rx, 1 = the unfused form.
+    The one-pass form on a slab of >= 4 planes runs as three launches (the
+    interior halves overlap the R and Y exchanges on the side stream, the
+    edge planes in between; CFD_HIP_RB_SPLIT=0: one launch between blocking
+    exchanges); 17^3 over 4 ranks mixes 4- and 3-plane slabs."""
+    monkeypatch.setenv("CFD_HIP_RB_SPLIT", split)
     g, rhs = cases.cos_rhs(17)
     xo = np.zeros_like(rhs)
     if maxit is None:
@@ -257,3 +264,70 @@ def test_slab_poisson_relax_bitwise(hip_lib, method, nranks, two_pass, maxit):
     assert all(s == so for s in stat)
     assert all(i == sto.iterations for i in its)
     np.testing.assert_array_equal(x, xo)
+
+
+@pytest.fixture()
+def omp_oracle():
+    import os
+    n = len(os.sched_getaffinity(0))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    oracle.set_threads(max(1, min(n, env) if env > 0 else n))
+    yield
+    oracle.set_threads(1)
+
+
+DEPTH_N = 130  # 128 interior planes: 16 per rank at 8 ranks
+
+
+def test_slab8_taylor_green_depth_vs_oracle(hip_lib, omp_oracle):
+    """8 ranks at a realistic slab depth (130^3: 16 planes each), so the CG's
+    split sweep B (edge planes + interior), the r halo on the side stream and
+    the x fold run on real slab interiors: fields within 1e-10 of the oracle,
+    CG iterations within 1 per step."""
+    g, f, p = cases.tg3(DEPTH_N)
+    S = Slabs(g, 8)
+    try:
+        S.scatter(f)
+        hist = _run_steps(S, g, p, 2, _tg_bc_device)
+        got = {k: S.gather(k) for k in FIELDS}
+    finally:
+        S.close()
+    ohist = _oracle_steps(g, f, p, 2, cases.tg3_bc, A.ORACLE_POISSON_CG)
+    for r in range(8):
+        assert hist[r] == hist[0]
+    for (ih, _, _), (io, _, _) in zip(hist[0], ohist):
+        assert ih > 50 and abs(ih - io) <= 1, (ih, io)
+    for k in FIELDS:
+        ref = getattr(f, k)
+        scale = max(1.0, float(np.max(np.abs(ref))))
+        assert float(np.max(np.abs(got[k] - ref))) / scale <= 1e-10, k
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_slab8_cavity_rbsor_depth_bitwise(hip_lib, omp_oracle, monkeypatch, split):
+    """8 ranks at 130^3 with the one-pass RB-SOR: the three-launch iteration
+    (interior halves overlapping the R / Y exchanges) on 16-plane slabs,
+    bitwise the oracle's red-black SOR step, iteration counts included."""
+    monkeypatch.setenv("CFD_HIP_RB_SPLIT", split)
+    g, f, p = cases.cavity(DEPTH_N, DEPTH_N, DEPTH_N, Re=100.0, dt=5e-4)
+    tol = 1e-3
+    S = Slabs(g, 8, poisson_method=A.HIP_POISSON_REDBLACK, poisson_tolerance=tol,
+              poisson_max_iter=5000)
+    try:
+        S.scatter(f)
+        hist = _run_steps(S, g, p, 2, _cavity_bc_device)
+        got = {k: S.gather(k) for k in FIELDS}
+    finally:
+        S.close()
+    oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=tol,
+                                                               max_iterations=5000))
+    try:
+        ohist = _oracle_steps(g, f, p, 2, lambda ff: api.cavity_bc(ff, 1.0),
+                              A.ORACLE_POISSON_REDBLACK)
+    finally:
+        oracle.set_projection_poisson_params(None)
+    for r in range(8):
+        assert hist[r] == ohist, (r, hist[r], ohist)
+    assert all(it > 10 for it, _, _ in ohist)
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], getattr(f, k), err_msg=k)
