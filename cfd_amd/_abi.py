@@ -143,6 +143,7 @@ class HipProjConfig(C.Structure):
         ("dirty_faces", C.c_int),
         ("dirty_sync_interval", C.c_int),
         ("cg_variant", C.c_int),
+        ("dirty_verify_interval", C.c_int),
     ]
 
 

@@ -178,6 +178,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_get_timing", None, V, A.c_double_p, P(C.c_longlong))
     _sig(lib, "hip_proj_synchronize", C.c_int, V)
     _sig(lib, "hip_proj_sync_host", C.c_int, V, P(A.FlowField))
+    _sig(lib, "hip_proj_mark_host_dirty", C.c_int, V)
     _sig(lib, "hip_proj_device_bytes", C.c_size_t, V)
     _sig(lib, "hip_proj_row_pitch", C.c_size_t, V)
     _sig(lib, "hip_proj_cg_fixed_iters", C.c_double, V, A.c_double_p, C.c_double, C.c_double,

@@ -288,6 +288,10 @@ class Solver:
     def init(self, grid: Grid, params: A.SolverParams) -> int:
         return _native.host().solver_init(self._ptr, grid.ptr, C.byref(params))
 
+    def mark_host_dirty(self):
+        """hip_proj_mark_host_dirty: the next host-buffer step uploads in full."""
+        _check(self._lib().hip_proj_mark_host_dirty(self._ctx), "hip_proj_mark_host_dirty")
+
     def step(self, field: FlowField, grid: Grid, params: A.SolverParams,
              stats: Optional[A.SolverStats] = None) -> int:
         st = stats if stats is not None else A.SolverStats()

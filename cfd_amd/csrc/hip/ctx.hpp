@@ -106,6 +106,11 @@ struct hip_proj_ctx {
     int resident = 0;
     const double* res_ptr[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     long long res_steps = 0;     // host steps since the last full download
+    // dirty_verify_interval: hash of the host arrays' interior as the last
+    // resident step left it (valid when hash_ok)
+    unsigned long long host_hash[5] = {0, 0, 0, 0, 0};   // deep interior (hash_ok)
+    unsigned long long host_hash1[5] = {0, 0, 0, 0, 0};  // layer 1, after the last step
+    int hash_ok = 0, hash_nf = 0;
     double* shell_dev = nullptr;  // packed shell staging (device / pinned host)
     double* shell_host = nullptr;
     size_t shell_cap = 0;
@@ -343,3 +348,8 @@ cfd_status_t ctx_shell_put(hip_proj_ctx* c, const double* const* host, double* c
                            int depth) __attribute__((visibility("hidden")));
 cfd_status_t ctx_shell_get(hip_proj_ctx* c, double* const* host, double* const* dev, int nf,
                            int depth) __attribute__((visibility("hidden")));
+// Position-weighted 64-bit hashes of each host array's deep interior (all
+// indices in [2, n-3]; layer1 = false) or of the layer next to the boundary
+// (layer1 = true), multithreaded (shell_io.hip).
+void ctx_host_hash(const hip_proj_ctx* c, const double* const* host, int nf, bool layer1,
+                   unsigned long long* out) __attribute__((visibility("hidden")));

@@ -1530,6 +1530,13 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     return CFD_SUCCESS;
 }
 
+cfd_status_t hip_proj_mark_host_dirty(hip_proj_ctx_t* c) {
+    if (!c) return CFD_ERROR_INVALID;
+    c->resident = 0;
+    c->hash_ok = 0;
+    return CFD_SUCCESS;
+}
+
 cfd_status_t hip_proj_step_device(hip_proj_ctx_t* c, const grid* g,
                                   const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
     if (c) c->resident = 0;
@@ -1566,6 +1573,26 @@ static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
     const bool same = c->resident && c->res_ptr[0] == f->u && c->res_ptr[1] == f->v &&
                       c->res_ptr[2] == f->w && c->res_ptr[3] == f->p &&
                       c->res_ptr[4] == f->T && (!f->T || c->T);
+    const int verify = c->cfg.dirty_verify_interval;
+    if (shell && same && verify > 0 && c->hash_ok && c->res_steps % verify == 0) {
+        // the guard: the interior of the host arrays must be what the
+        // resident steps left there (the device holds the current interior)
+        double* host[5];
+        double* dev[5];
+        const int nf = host_fields(c, f, host, dev);
+        unsigned long long h[5], h1[5];
+        ctx_host_hash(c, host, nf, false, h);
+        ctx_host_hash(c, host, nf, true, h1);
+        for (int q = 0; q < nf && q < c->hash_nf; ++q)
+            if (h[q] != c->host_hash[q] || h1[q] != c->host_hash1[q]) {
+                set_err(CFD_ERROR_INVALID,
+                        "projection_hip resident mode: the interior of a host field changed "
+                        "since the last step (it is not uploaded); call hip_proj_sync_host, "
+                        "write the cells, then hip_proj_mark_host_dirty");
+                return CFD_ERROR_INVALID;
+            }
+    }
+    const bool full_up = !(shell && same);
     if (shell && same) {
         double* host[5];
         double* dev[5];
@@ -1597,7 +1624,9 @@ static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
     if (s == CFD_SUCCESS || s == CFD_ERROR_DIVERGED || done > 0) {
         ++c->res_steps;
         const int every = c->cfg.dirty_sync_interval;
-        if (shell && s == CFD_SUCCESS && !(every > 0 && c->res_steps % every == 0)) {
+        const bool shell_down = shell && s == CFD_SUCCESS && !(every > 0 && c->res_steps % every == 0);
+        if (!shell_down) c->hash_ok = 0;  // the whole host field changed
+        if (shell_down) {
             double* host[5];
             double* dev[5];
             const int nall = host_fields(c, f, host, dev);
@@ -1613,6 +1642,7 @@ static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
     } else if (shell) {
         // nothing completed: the device holds the uploaded state; make the
         // whole host field current before handing the error back
+        c->hash_ok = 0;
         cfd_status_t d = hip_proj_download(c, f);
         if (d != CFD_SUCCESS) return d;
     }
@@ -1620,6 +1650,18 @@ static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
         c->resident = 1;
         c->res_ptr[0] = f->u, c->res_ptr[1] = f->v, c->res_ptr[2] = f->w, c->res_ptr[3] = f->p;
         c->res_ptr[4] = f->T;
+        if (verify > 0) {
+            // the guard's reference: layer 1 as this step's download left it;
+            // the deep interior only after a full transfer (it is untouched
+            // on the host otherwise)
+            double* host[5];
+            double* dev[5];
+            const int nf = host_fields(c, f, host, dev);
+            if (full_up || !c->hash_ok || c->hash_nf != nf) ctx_host_hash(c, host, nf, false, c->host_hash);
+            ctx_host_hash(c, host, nf, true, c->host_hash1);
+            c->hash_nf = nf;
+            c->hash_ok = 1;
+        }
     }
     if (s == CFD_SUCCESS && stats && f->T && !shell) {
         // compute_max_temperature (solver_registry.c:52-62) on the host copy
@@ -1663,6 +1705,16 @@ cfd_status_t hip_proj_sync_host(hip_proj_ctx_t* c, flow_field* f) {
     ST_TRY(hip_proj_download(c, f));
     if (c->resident && f->T && c->T) ST_TRY(hip_proj_get_field(c, HIP_FIELD_T, f->T));
     c->res_steps = 0;
+    c->hash_ok = 0;
+    if (c->resident && c->cfg.dirty_verify_interval > 0) {  // the guard's new reference
+        double* host[5];
+        double* dev[5];
+        const int nf = host_fields(c, f, host, dev);
+        ctx_host_hash(c, host, nf, false, c->host_hash);
+        ctx_host_hash(c, host, nf, true, c->host_hash1);
+        c->hash_nf = nf;
+        c->hash_ok = 1;
+    }
     return CFD_SUCCESS;
 }
 

@@ -199,3 +199,65 @@ cfd_status_t ctx_shell_get(hip_proj_ctx* c, double* const* host, double* const* 
     host_rows(m, nf, host, c->shell_host, false);
     return CFD_SUCCESS;
 }
+
+// Resident-mode guard (hip_proj_config_t.dirty_verify_interval): hashes of
+// the host arrays' cells inside the outer layer (the layer a caller's BC
+// routine writes), in two parts: the deep interior (every index in
+// [2, n-3]; the resident steps never write it on the host, so its hash holds
+// until a full download) and layer 1 (the cells next to the boundary, which
+// every step's depth-2 shell download rewrites, so its hash is retaken after
+// each step; shell-sized). Each cell contributes mix(bits) * (2 idx + 1), so
+// a sum is order-independent (summed per plane range over threads) and
+// changes when any value changes or two values swap.
+void ctx_host_hash(const hip_proj_ctx* c, const double* const* host, int nf, bool layer1,
+                   unsigned long long* out) {
+    const long long nx = (long long)c->nx, ny = (long long)c->ny, nz = (long long)c->nz;
+    const bool is3d = nz > 1;
+    const long long k0 = is3d ? 1 : 0, k1 = is3d ? nz - 1 : 1;
+    const long long planes = k1 - k0;
+    unsigned hc = std::thread::hardware_concurrency();
+    int nt = (int)std::min<unsigned>(hc ? hc : 1, 16);
+    if (const char* e = getenv("CFD_HIP_SHELL_THREADS")) nt = std::max(1, atoi(e));
+    if (layer1) nt = std::min(nt, 4);
+    nt = (int)std::max(1LL, std::min<long long>(nt, planes));
+    auto mix = [](const double* p, long long idx) {
+        unsigned long long b;
+        memcpy(&b, p, sizeof(b));
+        b ^= b >> 31;
+        b *= 0x9E3779B97F4A7C15ull;
+        return b * (unsigned long long)(2 * idx + 1);
+    };
+    for (int f = 0; f < nf; ++f) {
+        std::vector<unsigned long long> part(nt, 0ull);
+        auto work = [&](int t) {
+            unsigned long long h = 0;
+            for (long long k = k0 + planes * t / nt; k < k0 + planes * (t + 1) / nt; ++k) {
+                const bool kedge = is3d && (k == 1 || k == nz - 2);
+                for (long long j = 1; j < ny - 1; ++j) {
+                    const long long row = (k * ny + j) * nx;
+                    const bool edge_row = kedge || j == 1 || j == ny - 2;
+                    if (!layer1) {
+                        if (edge_row) continue;
+                        for (long long i = 2; i < nx - 2; ++i) h += mix(host[f] + row + i, row + i);
+                    } else if (edge_row) {
+                        for (long long i = 1; i < nx - 1; ++i) h += mix(host[f] + row + i, row + i);
+                    } else {
+                        h += mix(host[f] + row + 1, row + 1);
+                        h += mix(host[f] + row + nx - 2, row + nx - 2);
+                    }
+                }
+            }
+            part[t] = h;
+        };
+        if (nt == 1) {
+            work(0);
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+            for (auto& t : th) t.join();
+        }
+        unsigned long long h = 0;
+        for (auto v : part) h += v;
+        out[f] = h;
+    }
+}

@@ -104,6 +104,14 @@ typedef struct {
                                      products of an iteration in ONE reduction (one
                                      all-reduce per iteration on Z-slabs), same stopping rule
                                      and stats, iterates equal to rounding only */
+    int dirty_verify_interval;    /* resident mode guard: every N-th resident step first
+                                     checks that the caller left the interior of its host
+                                     arrays (every cell but the outer layer) as the last
+                                     step did (a 64-bit position-weighted hash, two
+                                     multithreaded host passes every N steps). A changed
+                                     interior fails the step with CFD_ERROR_INVALID before
+                                     anything runs; the device state is kept. 0 = off
+                                     (default). */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;
@@ -161,6 +169,12 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_step(hip_proj_ctx_t* ctx, flow_field* field
  * resident) to the caller's field, so that every host cell is current. A
  * no-op copy of the full fields otherwise. */
 CFD_HIP_EXPORT cfd_status_t hip_proj_sync_host(hip_proj_ctx_t* ctx, flow_field* field);
+
+/* Resident mode: the caller declares that its host arrays hold the state to
+ * use (it re-initialised them, restored a checkpoint into them, or wrote
+ * interior cells after hip_proj_sync_host); the next host-buffer step uploads
+ * them in full. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_mark_host_dirty(hip_proj_ctx_t* ctx);
 
 /* Device-resident path. */
 CFD_HIP_EXPORT cfd_status_t hip_proj_upload(hip_proj_ctx_t* ctx, const flow_field* field);

@@ -175,3 +175,59 @@ def test_plugin_env_switch(hip_lib, monkeypatch):
         assert same == (step % 2 == 1), step
     s_res.close()
     s_full.close()
+
+
+@pytest.mark.parametrize("verify,cell", [(1, (10, 10, 10)), (1, (1, 7, 9)), (2, (10, 10, 10))])
+def test_verify_guard_and_mark_host_dirty(hip_lib, verify, cell):
+    """dirty_verify_interval: a caller that writes an interior cell of its
+    host arrays between resident steps (which the shell upload would ignore)
+    gets CFD_ERROR_INVALID from the next verified step, nothing run. The
+    supported way -- hip_proj_sync_host, write, hip_proj_mark_host_dirty --
+    then gives bitwise the full-transfer run with the same write. Deep cells
+    are caught at the next verified step whatever the interval; cell (1, 7, 9)
+    is in the layer next to the boundary, which every step's download
+    rewrites, caught with interval 1."""
+    g, f, p = cases.cavity(33, 29, 21, Re=100.0, dt=5e-4)
+    fr = _clone(g, f)
+    full = api.HipProjection(g.nx, g.ny, g.nz)
+    res = api.HipProjection(g.nx, g.ny, g.nz, dirty_faces=1, dirty_verify_interval=verify)
+    try:
+        for _ in range(3):
+            _cavity_bc(f)
+            _cavity_bc(fr)
+            assert full.step(f, g, p) == A.CFD_SUCCESS
+            assert res.step(fr, g, p) == A.CFD_SUCCESS
+        before = fr.u.copy()
+        fr.u[cell] += 0.25
+        statuses = []
+        for _ in range(verify):  # the write is caught within `verify` steps
+            _cavity_bc(fr)
+            s = res.step(fr, g, p)
+            statuses.append(s)
+            if s != A.CFD_SUCCESS:
+                break
+        assert statuses[-1] == A.CFD_ERROR_INVALID, statuses
+        assert "interior" in api._native.last_error()
+        n_ok = len(statuses) - 1  # verified-free steps that ran before the check
+        for _ in range(n_ok):
+            _cavity_bc(f)
+            assert full.step(f, g, p) == A.CFD_SUCCESS
+        # the supported path: sync, write, mark dirty
+        res.sync_host(fr)
+        for k in FIELDS[:4]:
+            np.testing.assert_array_equal(getattr(fr, k), getattr(f, k), err_msg=k)
+        f.u[cell] += 0.25
+        fr.u[cell] += 0.25
+        res.mark_host_dirty()
+        for _ in range(2):
+            _cavity_bc(f)
+            _cavity_bc(fr)
+            assert full.step(f, g, p) == A.CFD_SUCCESS
+            assert res.step(fr, g, p) == A.CFD_SUCCESS
+        res.sync_host(fr)
+        for k in FIELDS[:4]:
+            np.testing.assert_array_equal(getattr(fr, k), getattr(f, k), err_msg=k)
+        assert not np.array_equal(before, fr.u)
+    finally:
+        full.close()
+        res.close()
