@@ -73,8 +73,10 @@ def parse():
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--dt", type=float, default=1e-4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-cg-iters", type=int, default=100,
-                    help="CG iterations timed in the CPU baseline sample")
+    ap.add_argument("--cpu-cg-iters", type=int, default=40,
+                    help="CG iterations timed in each CPU baseline sample")
+    ap.add_argument("--cpu-repeat", type=int, default=3,
+                    help="CPU baseline samples per placement (the median is reported)")
     ap.add_argument("--cpu-scalar-cg-iters", type=int, default=5,
                     help="CG iterations in the 1-thread CPU sample (0: skip it)")
     ap.add_argument("--cpu-timeout", type=int, default=420,
@@ -565,7 +567,8 @@ def cpu_baseline(n, args, k_gpu):
     16; the mask still shows all 256). Two placements, since the host is
     shared with other boxes: OMP_PROC_BIND=close OMP_PLACES=cores (threads on
     the first cores of the mask) and unbound (the OS picks idle CPUs); the
-    faster is the reported value, both are recorded."""
+    faster median is the reported value, both are recorded with the min and
+    max of their `cpu_repeat` samples."""
     import subprocess
 
     affinity = len(os.sched_getaffinity(0))
@@ -579,7 +582,7 @@ def cpu_baseline(n, args, k_gpu):
             env.pop("OMP_PLACES", None)
         cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--size", str(n), "--dt",
                str(args.dt), "--re", str(args.re), "--k-gpu", str(k_gpu), "--cg-iters",
-               str(args.cpu_cg_iters),
+               str(args.cpu_cg_iters), "--repeat", str(args.cpu_repeat),
                "--scalar-cg-iters", str(args.cpu_scalar_cg_iters if name == "bound" else 0)]
         try:
             r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
@@ -597,7 +600,8 @@ def cpu_baseline(n, args, k_gpu):
     best = max(ok, key=lambda k: ok[k]["value"])
     out = dict(ok[best])
     out["placement"] = best
-    out["placements"] = {k: {"value": v.get("value"), "cg_iter_ms": v.get("cg_iter_ms"),
+    out["placements"] = {k: {"value": v.get("value"), "min": v.get("min"), "max": v.get("max"),
+                             "runs": v.get("runs"), "cg_iter_ms": v.get("cg_iter_ms"),
                              "error": v.get("error")} for k, v in runs.items()}
     if "scalar_1core" not in out and "bound" in ok:
         out["scalar_1core"] = ok["bound"].get("scalar_1core")

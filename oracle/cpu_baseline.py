@@ -10,8 +10,12 @@ one 512^3 lid-driven cavity step from rest, predictor + divergence +
 corrector in full, the first `cg_iters` CG iterations timed and scaled to the
 GPU's iterations per step. Prints one JSON object.
 
+The sample is repeated `--repeat` times (fresh fields each time); the value
+is the median, with the min and max beside it (the GPU pool's hosts are
+shared, and one sample swung 41 % between boxes in round 2).
+
 usage: python -m oracle.cpu_baseline --size N --dt DT --re RE --k-gpu K
-                                     --cg-iters C [--scalar-cg-iters S]
+                                     --cg-iters C [--scalar-cg-iters S] [--repeat R]
 """
 from __future__ import annotations
 
@@ -45,6 +49,7 @@ def main():
     ap.add_argument("--k-gpu", type=float, required=True)
     ap.add_argument("--cg-iters", type=int, default=100)
     ap.add_argument("--scalar-cg-iters", type=int, default=0)
+    ap.add_argument("--repeat", type=int, default=3)
     a = ap.parse_args()
     affinity = len(os.sched_getaffinity(0))  # before OpenMP binds this thread
 
@@ -72,13 +77,19 @@ def main():
         t_step = (ph[0] + ph[1] + ph[3]) / 1e3 + a.k_gpu * t_cg_iter
         return s, it, wall, t_cg_iter, t_step
 
-    s, it, wall, t_cg_iter, t_step = sample(threads, a.cg_iters)
+    runs = [sample(threads, a.cg_iters) for _ in range(max(1, a.repeat))]
+    vals = sorted(n_int / r[4] / 1e6 for r in runs)
+    med = vals[len(vals) // 2]
+    s, it, wall, t_cg_iter, t_step = min(runs, key=lambda r: abs(n_int / r[4] / 1e6 - med))
     # CG iteration bytes as the survey credits them (80 B/cell)
-    out = {"value": round(n_int / t_step / 1e6, 4), "unit": "MLUPS", "cores": threads,
+    out = {"value": round(med, 4), "unit": "MLUPS", "cores": threads,
            "kind": "port",
-           "sample": (f"{n}^3 cavity step 1 on the host: predictor+divergence+corrector timed "
-                      f"in full, {it} CG iterations timed ({t_cg_iter*1e3:.1f} ms/iter) and "
-                      f"scaled to the GPU's {a.k_gpu:.0f} iterations/step; OpenMP x{threads} "
+           "runs": [round(v, 4) for v in vals], "min": round(vals[0], 4),
+           "max": round(vals[-1], 4),
+           "sample": (f"{n}^3 cavity step 1 on the host, {len(runs)} times (median reported): "
+                      f"predictor+divergence+corrector timed in full, {it} CG iterations "
+                      f"timed ({t_cg_iter*1e3:.1f} ms/iter) and scaled to the GPU's "
+                      f"{a.k_gpu:.0f} iterations/step; OpenMP x{threads} "
                       f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
                       f"OMP_PLACES={os.environ.get('OMP_PLACES')}); sample wall {wall:.1f} s"),
            "cg_iter_ms": round(t_cg_iter * 1e3, 2),
