@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--relax-max-iter", type=int, default=20000,
                     help="convection: RB-SOR iteration cap per step (the 1024^2 x 512 solve "
                          "needs ~13 000; the reference's default 5000 would fail the step)")
+    ap.add_argument("--relax-tol", type=float, default=1e-6,
+                    help="convection: RB-SOR relative tolerance (the reference default 1e-6)")
     ap.add_argument("--dump", default="",
                     help="convection: write each rank's owned planes to DUMP.rank<r>.npz")
     ap.add_argument("--re", type=float, default=1000.0)
@@ -434,7 +436,8 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
     g, p, T0 = convection_setup(nx, ny, nz)
     ctx = api.HipProjection(nx, ny, nz, comm=comm, device=local,
                             poisson_method=A.HIP_POISSON_REDBLACK,
-                            poisson_max_iter=args.relax_max_iter, relax_two_pass=0)
+                            poisson_max_iter=args.relax_max_iter,
+                            poisson_tolerance=args.relax_tol, relax_two_pass=0)
     for fid in (A.HIP_FIELD_U, A.HIP_FIELD_V, A.HIP_FIELD_W, A.HIP_FIELD_P):
         ctx.fill(fid, 0.0)
     ctx.set_field(A.HIP_FIELD_T, np.broadcast_to(T0[None, None, :], ctx.shape))
@@ -515,7 +518,7 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
             "config": {"workload": f"{nx}x{ny}x{nz} natural convection Ra=1e3, Pr=0.71, "
                                    "projection_hip with the one-pass RB-SOR pressure solve",
                        "grid": [nx, ny, nz], "interior_cells": n_int,
-                       "relax_max_iter": args.relax_max_iter,
+                       "relax_max_iter": args.relax_max_iter, "relax_tol": args.relax_tol,
                        "parallelism": f"z-slab x{world} (RCCL halo)" if world > 1
                                       else "single GPU"},
             "rbsor_iters_per_step": iters,

@@ -288,10 +288,6 @@ class Solver:
     def init(self, grid: Grid, params: A.SolverParams) -> int:
         return _native.host().solver_init(self._ptr, grid.ptr, C.byref(params))
 
-    def mark_host_dirty(self):
-        """hip_proj_mark_host_dirty: the next host-buffer step uploads in full."""
-        _check(self._lib().hip_proj_mark_host_dirty(self._ctx), "hip_proj_mark_host_dirty")
-
     def step(self, field: FlowField, grid: Grid, params: A.SolverParams,
              stats: Optional[A.SolverStats] = None) -> int:
         st = stats if stats is not None else A.SolverStats()
@@ -494,6 +490,10 @@ class HipProjection:
         st = stats if stats is not None else A.SolverStats()
         return self._lib().hip_proj_step(self._ctx, field.ptr, grid.ptr, C.byref(params),
                                          C.byref(st))
+
+    def mark_host_dirty(self):
+        """hip_proj_mark_host_dirty: the next host-buffer step uploads in full."""
+        _check(self._lib().hip_proj_mark_host_dirty(self._ctx), "hip_proj_mark_host_dirty")
 
     def step_device(self, grid: Grid, params: A.SolverParams,
                     stats: Optional[A.SolverStats] = None) -> int:

@@ -517,12 +517,16 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                                       it));
                 HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
             } else {
+                // same collective order as the split form (R halo, Y halo,
+                // residual max): the in-process group pairs its ranks' calls
+                // by order, and a slab of < 4 planes runs this form beside
+                // split neighbours
                 ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {RH}); }, it));
                 rb1(c->rgeo);
+                ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {xo}); }, it));
                 if (!mb)
                     ST_TRY(timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] { return finish(it); },
                                       it));
-                ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {xo}); }, it));
             }
         } else if (single) {
             // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the

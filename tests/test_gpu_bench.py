@@ -79,7 +79,7 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
     assert cmp["cg_variant"] == 1 and cmp["cg_iters"] > 0 and cmp["ms_per_cg_iter_wall"] > 0
 
 
-def _oracle_convection(nx, ny, nz, steps):
+def _oracle_convection(nx, ny, nz, steps, tol):
     """The oracle's run of bench.convection_setup: RB-SOR projection steps
     with the energy equation (solver_projection.c:46-297 with the RB-SOR
     solve, energy_solver.c:21-334)."""
@@ -96,7 +96,8 @@ def _oracle_convection(nx, ny, nz, steps):
     f.u[...] = f.v[...] = f.w[...] = f.p[...] = 0.0
     f.rho[...] = 1.0
     f.T[...] = np.broadcast_to(T0[None, None, :], f.T.shape)
-    oracle.set_projection_poisson_params(oracle.poisson_params(max_iterations=20000))
+    oracle.set_projection_poisson_params(oracle.poisson_params(tolerance=tol,
+                                                               max_iterations=20000))
     its = []
     try:
         for _ in range(steps):
@@ -111,14 +112,17 @@ def _oracle_convection(nx, ny, nz, steps):
 @pytest.mark.parametrize("world", [1, 2])
 def test_bench_convection_launcher_bitwise(hip_lib, tmp_path, world):
     """configs[4]'s launcher (bench.py --case convection): 1 rank, and 2 ranks
-    over RCCL (shared device), at 24 x 20 x 18; every rank's owned planes
-    of u, v, w, p, T and the RB-SOR iteration counts bitwise the oracle's."""
+    over RCCL (shared device), at 24 x 24 x 18 with the RB-SOR tolerance
+    at 1e-3 (this small Neumann problem stalls above 1e-6); every rank's
+    owned planes of u, v, w, p, T and the RB-SOR iteration counts bitwise
+    the oracle's."""
     import numpy as np
 
     nx, nz, steps = 24, 18, 2
     dump = tmp_path / "conv"
     args = ["bench.py", "--gpus", str(world), "--case", "convection", "--size", str(nx),
-            "--nz", str(nz), "--steps", str(steps), "--warmup", "0", "--dump", str(dump)]
+            "--nz", str(nz), "--steps", str(steps), "--warmup", "0", "--relax-tol", "1e-3",
+            "--dump", str(dump)]
     env = _env()
     if world > 1:
         env["CFD_BENCH_SHARED_GPU"] = "1"
@@ -138,7 +142,8 @@ def test_bench_convection_launcher_bitwise(hip_lib, tmp_path, world):
             assert q["relax_halo_ms_per_iter"] > 0
     if world == 1:
         assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["kernel"].startswith("k_rb1<")
-    fo, its = _oracle_convection(nx, nx, nz, steps)
+    fo, its = _oracle_convection(nx, nx, nz, steps, 1e-3)
+    assert all(i > 10 for i in its)
     assert d["rbsor_iters_per_step"] == its
     got = {k: np.full((nz, nx, nx), np.nan) for k in ("u", "v", "w", "p", "T")}
     for rk in range(world):
