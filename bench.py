@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--size", type=int, default=512, help="grid points per axis")
+    ap.add_argument("--size", type=int, default=0,
+                    help="grid points per axis (default 512; convection: 1024 x 1024 x 512)")
     ap.add_argument("--case", choices=("cavity", "tg", "convection"), default="cavity",
                     help="cavity: configs[2] (default, every N); tg: configs[3] Taylor-Green; "
                          "convection: configs[4] natural convection with RB-SOR")
@@ -126,6 +127,8 @@ def main():
         raise SystemExit("bench: no HIP device")
     torch.cuda.set_device(local)
 
+    if args.size <= 0:
+        args.size = 1024 if args.case == "convection" else 512
     n = args.size
     if args.case == "convection":
         comm = None

@@ -2286,7 +2286,8 @@ template <int FL, int TC, bool PF, bool DIST = false>
 static __global__ __launch_bounds__(1024, 4) void k_rb1(
     SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
     const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
-    const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred) {
+    const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred,
+    int neu) {
     constexpr int NW = 16;  // waves
     constexpr int TR = rb1_rows<TC>();
     constexpr int OX = rb1_ox<TC>(), OY = rb1_oy<TC>();
@@ -2348,6 +2349,11 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
     const bool wr = (TC == 64) ? (r >= 1 && r <= TR - 2) : true;
     const bool wo = (TC == 64) ? orow : true;
     const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
+    // the folded Neumann shell (neu): this lane's x-face roles and whether it
+    // stores (pairs (nx-1, pad) of odd nx leave cell nx-1 to role 4)
+    const int nrole = (i0 == 0 ? 1 : 0) | (i0 + 1 == g.nx - 1 ? 2 : 0) |
+                      (i0 + 1 == g.nx - 2 ? 4 : 0) |
+                      ((own && jin && i0 <= g.nx - 2) ? 8 : 0);
     // Loads are issued unconditionally from clamped (always valid) addresses
     // and never masked: with the same loads on every control path and no
     // select right behind them, the compiler's vmcnt counting waits for a
@@ -2450,7 +2456,39 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
                 const double v = sor1(rc, DivC{}, rm.y, rm.x, rlr, rys.y, ryn.y, rmmh, R.y, bmh);
                 if (own && in1) out.y = v;
             }
-            if (own && ld && jin) st2v<FL>(Y, (long long)q * g.ps + col, out);
+            if (neu) {
+                // the iteration's Neumann BC (linear_solver_redblack.c:139) folded
+                // into the stores: every boundary cell of Y is the gather
+                // k_bc_shell / k_rx_shell mode 1 makes, Y at the clamped-inward
+                // position (bc_map), so the writer of that source cell stores
+                // it to its mirror positions too: x faces within the pair (or
+                // one 8-B store when nx is odd), y faces as a copy of rows 1 /
+                // ny-2, z faces (global, not a slab's halo) as copies of
+                // planes k0 / k1-1
+                // nrole (lane constant): 1 = pair (0, 1), 2 = pair (nx-2, nx-1),
+                // 4 = nx odd and .y is cell nx-2 (cell nx-1 <- .y), 8 = store
+                if (nrole & 1) out.x = out.y;
+                if (nrole & 2) out.y = out.x;
+                if (nrole & 8) {
+                    // j is wave-uniform with TC = 64 (one row per wave), so
+                    // are q and the z-face tests: scalar branches
+                    auto put = [&](long long base) __attribute__((always_inline)) {
+                        st2v<FL>(Y, base, out);
+                        if (nrole & 4) Y[base + 2] = out.y;
+                        if (j == 1 || j == g.ny - 2) {
+                            const long long b2 = base + (j == 1 ? -g.px : g.px);
+                            st2v<FL>(Y, b2, out);
+                            if (nrole & 4) Y[b2 + 2] = out.y;
+                        }
+                    };
+                    const long long base = (long long)q * g.ps + col;
+                    put(base);
+                    if (q == g.k0 && !rh_lo) put(base - g.ps);
+                    if (q == g.k1 - 1 && !rh_hi) put(base + g.ps);
+                }
+            } else if (own && ld && jin) {
+                st2v<FL>(Y, (long long)q * g.ps + col, out);
+            }
         }
         // step q + 1 updates the .x cell iff this step did not
         rmmh = E ? rm.y : rm.x;

@@ -455,6 +455,11 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     // colour sweeps of k_rx
     const bool single = method == HIP_POISSON_REDBLACK && c->nz > 1 &&
                         c->cfg.relax_two_pass == 0;
+    // k_rb1 writes the iteration's Neumann shell itself (no k_rx_shell);
+    // CFD_HIP_RB1_FOLD=0 keeps the separate shell launch (A/B)
+    static const bool fold_env = !(getenv("CFD_HIP_RB1_FOLD") &&
+                                   atoi(getenv("CFD_HIP_RB1_FOLD")) == 0);
+    const bool neu_fold = single && fold_env && c->poisson_bc == HIP_POISSON_BC_NEUMANN;
     const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
     ST_TRY(halo(c, {c->pn}));
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
@@ -485,7 +490,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                                           c->stream, c->ta, c->tb, 0, sg, rc, xi, xo, c->rhs,
                                           c->rxst, c->partials, c->counter, it, (const double*)RH,
                                           c->geo.lo_face ? 0 : 1, c->geo.hi_face ? 0 : 1, mb,
-                                          dred);
+                                          dred, neu_fold ? 1 : 0);
                 }, it);
             };
             // exchange of `f`'s edge planes on the side stream (halo
@@ -537,7 +542,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     hipExtLaunchKernelGGL((k_rb1<FL, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
                           c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
                           c->counter, it, (const double*)nullptr, 0, 0, (Mbox*)nullptr,        \
-                          (unsigned long long*)nullptr)
+                          (unsigned long long*)nullptr, neu_fold ? 1 : 0)
             timed(c, HIP_KT_RELAX, [&] {
                 if (!rb1_pf) RB1_LAUNCH(64, false);
                 else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
@@ -556,15 +561,17 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             sweep(RX_JACOBI, xi, xo, it);
             ST_TRY(finish(it));
         }
-        if (!(single && D))
+        if (D && !single)
             ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {xo}); }, it));
         // the iteration's apply_bc: Neumann (linear_solver_redblack.c:139,
         // linear_solver_jacobi.c:118), or the caller's fixed boundary values,
         // or x's own boundary kept
-        const double* shell_src = (c->poisson_bc == HIP_POISSON_BC_FIXED) ? c->bcfix : xi;
-        const int shell_mode = (c->poisson_bc == HIP_POISSON_BC_NEUMANN) ? 1 : 0;
-        hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
-                              c->tb, 0, c->geo, c->rxst, shell_src, xo, shell_mode);
+        if (!neu_fold) {
+            const double* shell_src = (c->poisson_bc == HIP_POISSON_BC_FIXED) ? c->bcfix : xi;
+            const int shell_mode = (c->poisson_bc == HIP_POISSON_BC_NEUMANN) ? 1 : 0;
+            hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream,
+                                  c->ta, c->tb, 0, c->geo, c->rxst, shell_src, xo, shell_mode);
+        }
         return CFD_SUCCESS;
     };
     // iterations 0..max_iter: sweep it also yields the residual after it - 1
