@@ -1,0 +1,107 @@
+"""BASELINE configs[2] at its own size: the bench's 512^3 lid-driven cavity
+trajectory (Re = 1000, dt = 1e-4, from rest, lid u = 1 on y = 1, the
+reference's CG settings) against the oracle's run of the same steps,
+committed as fixtures by tests/golden/make_golden.py cavity512 (the OpenMP
+oracle, solver_projection.c:46-297 with cg_scalar_solve's loop,
+linear_solver_cg.c:290-461; about 2.5 h on 8 cores).
+
+The device path is driven exactly as bench.py drives it: fields filled on
+the device, the caller BCs applied once (the step keeps the boundary faces),
+projection_hip steps on the resident fields. Per step: CG iterations within
+1 (the dot products are summed in another order), the initial CG residual
+within 1e-6 relative and the final one within 1e-4 (it is 1e-6 of the
+initial one, after ~1000 recursive updates), the interior L2 norm and max |.| of u, v,
+w, p within 1e-9 relative; after steps 1, 6 and 25 the sampled planes
+k = 1, 255, 510 (a stride-4 lattice, rows j = 1, 255, 509, 510, columns
+i = 1, 255, 510) within 1e-9 of the field's largest interior value. The reference's
+own backend-consistency bar is 1e-3 (tests/validation/test_cavity_backends.c:43)."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from cfd_amd import _abi as A
+from cfd_amd import api
+
+pytestmark = pytest.mark.gpu
+
+GOLD = Path(__file__).resolve().parent / "golden"
+N = 512
+REL = 1e-9
+
+
+def _fixture():
+    f = GOLD / f"cavity{N}_re1000_steps.json"
+    if not f.exists():
+        pytest.skip("512^3 fixture not generated (tests/golden/make_golden.py cavity512)")
+    return json.loads(f.read_text())
+
+
+def _interior_norms(a):
+    import torch
+    t = torch.from_numpy(a)[1:-1, 1:-1, 1:-1]
+    return float(torch.linalg.vector_norm(t)), float(t.abs().max())
+
+
+@pytest.mark.timeout(900)
+def test_cavity512_trajectory_vs_oracle(hip_lib):
+    rec = _fixture()
+    steps = rec["steps"]
+    g = api.Grid(N, N, N, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
+    params = api.validation_params(rec["dt"], 1.0 / rec["re"])
+    ctx = api.HipProjection(N, N, N)
+    fids = {"u": A.HIP_FIELD_U, "v": A.HIP_FIELD_V, "w": A.HIP_FIELD_W, "p": A.HIP_FIELD_P}
+    try:
+        for fid in fids.values():
+            ctx.fill(fid, 0.0)
+        ctx.set_density(1.0)
+        ctx.apply_dirichlet(A.HIP_FIELD_U, api.dirichlet(top=1.0))
+        ctx.apply_dirichlet(A.HIP_FIELD_V, api.dirichlet())
+        ctx.apply_dirichlet(A.HIP_FIELD_W, api.dirichlet())
+        ctx.apply_scalar_bc(A.HIP_FIELD_P, A.BC_TYPE_NEUMANN)
+        its = []
+        for row in steps:
+            st = A.SolverStats()
+            s = ctx.step_device(g, params, st)
+            assert s == A.CFD_SUCCESS, (row["step"], s, api._native.last_error())
+            ps = ctx.poisson_stats()
+            its.append((ps.iterations, row["cg_iters"]))
+            assert abs(ps.iterations - row["cg_iters"]) <= 1, (row["step"], its)
+            assert ps.initial_residual == pytest.approx(row["initial_residual"], rel=1e-6)
+            # the final residual is the recursively updated r after ~1000
+            # iterations, 1e-6 of the initial one: its rounding differs at
+            # ~1e-6 relative (1e-12 of the initial residual)
+            assert ps.final_residual == pytest.approx(row["final_residual"], rel=1e-4)
+            assert st.max_velocity == pytest.approx(row["max_velocity"], rel=REL)
+            assert st.max_pressure == pytest.approx(row["max_pressure"], rel=REL)
+            snap = GOLD / f"cavity{N}_re1000_step{row['step']}_planes.npz"
+            for k, fid in fids.items():
+                a = ctx.get_field(fid)
+                l2, mx = _interior_norms(a)
+                ol2, omx = row["norms"][k]
+                assert l2 == pytest.approx(ol2, rel=REL, abs=1e-300), (row["step"], k)
+                assert mx == pytest.approx(omx, rel=REL, abs=1e-300), (row["step"], k)
+                if snap.exists():
+                    z = np.load(snap)
+                    for kz in (1, 255, 510):
+                        pre = f"{k}_k{kz}_"
+                        plane = a[kz]
+                        # the field's scale (its interior max |.|): w on the
+                        # mid-plane k = 255 is ~0 by the z symmetry
+                        scale = max(float(z[pre + "stats"][2]), omx, 1e-300)
+                        li = z[pre + "lattice_idx"]
+                        got = {"lattice": plane[np.ix_(li, li)],
+                               "rows": plane[z[pre + "rows_j"], :],
+                               "cols": plane[:, z[pre + "cols_i"]].T}
+                        for part, val in got.items():
+                            d = float(np.max(np.abs(val - z[pre + part]))) / scale
+                            assert d <= REL, (row["step"], k, kz, part, d)
+                        s_sum, s_l2, s_max = z[pre + "stats"]
+                        assert float(np.sqrt(np.sum(plane * plane))) == pytest.approx(
+                            s_l2, rel=REL, abs=1e-300)
+                        assert float(np.max(np.abs(plane))) == pytest.approx(
+                            s_max, rel=REL, abs=1e-300)
+    finally:
+        ctx.close()
+    print("cavity512 CG iterations (device, oracle):", its)
