@@ -66,6 +66,11 @@ struct hip_proj_ctx {
     // interior part 2 (overlaps the exchange of the new iterate's edge planes)
     SGeo rg_in1{}, rg_edge{}, rg_in2{};
     int split_rb = 0;
+    // one device: k_rb1's full-width (TC 64) tiles stop at x = 124 T, and the
+    // remaining columns run as a strip of narrow tiles (TC 16 / 32) in a
+    // second launch sharing the residual reduction (rb_strip_tc 0: none)
+    SGeo rg_main{}, rg_strip{};
+    int rb_strip_tc = 0;
     int rb1_tc = 64;           // k_rb1 tile width in x pairs (64, 32, 16)
     SGeo pgeo{};               // predictor / corrector z-march tiling (k_pred2, k_corr2)
     int split_b = 0;

@@ -408,6 +408,9 @@ struct SGeo {
     // kmode 2 (k_rb1 on slabs): tiles cover planes [kt0, kt1) only, while
     // k0 / k1 still bound the planes that are updated
     int kt0, kt1;
+    // k_rb1: x of the first tile's first output column (the narrow
+    // remainder strip starts where the full-width tiles end)
+    int xofs;
 };
 
 __device__ __forceinline__ int xcd_tile(int b, int nt) {
@@ -2282,12 +2285,24 @@ constexpr int rb1_oy() { return 1024 / TC - 4; }  // output rows per tile
 // beforehand (k_rb_edge_r + halo); it cannot be formed here, since that needs
 // X two planes beyond the halo. The L-inf residual leaves as in k_rx: the
 // device mailbox's max, or dred for an RCCL max all-reduce + k_rx_finish.
-template <int FL, int TC, bool PF, bool DIST = false>
-static __global__ __launch_bounds__(1024, 4) void k_rb1(
-    SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
-    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
-    const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred,
-    int neu) {
+// LDS of one k_rb1 workgroup: X and R rows of two plane parities (the same
+// 64 KB for every tile width), the waves' residual maxima and the
+// last-workgroup flag.
+struct Rb1Lds {
+    double xb[2 * 1024 * 2];
+    double rb[2 * 1024 * 2];
+    double sh[16];
+    int flag;
+};
+
+// The body of k_rb1 for the tile width TC; bid = this workgroup's tile-block
+// index within its geometry g (k_rb1m runs two geometries in one grid).
+template <int FL, int TC, bool PF, bool DIST>
+__device__ __forceinline__ void rb1_body(
+    Rb1Lds& L, int bid, SGeo g, RelaxCoef rc, const double* __restrict__ X,
+    double* __restrict__ Y, const double* __restrict__ rhs, RxState* st, double* partials,
+    unsigned* counter, int it, const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb,
+    unsigned long long* dred, int neu) {
     constexpr int NW = 16;  // waves
     constexpr int TR = rb1_rows<TC>();
     constexpr int OX = rb1_ox<TC>(), OY = rb1_oy<TC>();
@@ -2295,8 +2310,10 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
     // its TC .y cells, so a pair is one ds_read2/ds_write2_b64 and an x
     // neighbour (one double of the adjacent lane) a conflict-free ds_read_b64
     // (with double2 rows those 8-B reads at a 16-B lane stride conflicted)
-    __shared__ double xb[2][TR][2][TC];
-    __shared__ double rb[2][TR][2][TC];
+    auto& xb = *reinterpret_cast<double(*)[2][TR][2][TC]>(L.xb);
+    auto& rb = *reinterpret_cast<double(*)[2][TR][2][TC]>(L.rb);
+    auto& sh = L.sh;
+    auto& flag = L.flag;
     auto lget = [&](double (&a)[2][TR][2][TC], int p, int r, int l) __attribute__((always_inline)) {
         return make_double2(a[p][r][0][l], a[p][r][1][l]);
     };
@@ -2305,11 +2322,9 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
         a[p][r][0][l] = v.x;
         a[p][r][1][l] = v.y;
     };
-    __shared__ double sh[NW];
-    __shared__ int flag;
     if (st->done) return;
     const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
-    const int t = xcd_tile(blockIdx.x, nt);
+    const int t = xcd_tile(bid, nt);
     const int tx = t % g.tiles_x;
     const int rest = t / g.tiles_x;
     const int ty = rest % g.tiles_y;
@@ -2320,7 +2335,7 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
     const int r = w + NW * (lane / TC);          // tile row
     const int cm = max(c - 1, 0), cp = min(c + 1, TC - 1);  // x neighbours' pairs
     const int rlo = max(r - 1, 0), rhi = min(r + 1, TR - 1);  // y neighbours' rows
-    const int i0 = tx * OX - 2 + 2 * c;  // even; the pair is (i0, i0 + 1)
+    const int i0 = g.xofs + tx * OX - 2 + 2 * c;  // even; the pair is (i0, i0 + 1)
     const int j = ty * OY - 2 + r;       // grid row
     // kmode 1: the slab's two edge planes (tz 0 -> k0, tz 1 -> k1 - 1);
     // kmode 2: the planes [kt0, kt1); else [k0, k1). A march over a plane
@@ -2576,6 +2591,38 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
             dred[0] = ord_enc(tot);
         }
     }
+}
+
+template <int FL, int TC, bool PF, bool DIST = false>
+static __global__ __launch_bounds__(1024, 4) void k_rb1(
+    SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
+    const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
+    const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred,
+    int neu) {
+    __shared__ Rb1Lds L;
+    rb1_body<FL, TC, PF, DIST>(L, blockIdx.x, g, rc, X, Y, rhs, st, partials, counter, it, RH,
+                               rh_lo, rh_hi, mb, dred, neu);
+}
+
+// One device, one launch: the full-width (TC 64) tiles of g64 in blocks
+// [0, nb64) and the narrow strip of the columns past them (g2, tile width
+// TC2) in the rest. A row's last TC-64 tile would be partial unless 124
+// divides it, and costs a full tile's steps for its few columns (512^3: 14
+// of 124); the strip's TC-16 / TC-32 tiles are 60 / 28 rows tall, so the
+// column strip needs 4.8x / 2.2x fewer workgroups. Both geometries share the
+// grid-wide residual reduction (part_total 0: gridDim.x workgroups).
+template <int FL, int TC2>
+static __global__ __launch_bounds__(1024, 4) void k_rb1m(
+    SGeo g64, SGeo g2, int nb64, RelaxCoef rc, const double* __restrict__ X,
+    double* __restrict__ Y, const double* __restrict__ rhs, RxState* st, double* partials,
+    unsigned* counter, int it, int neu) {
+    __shared__ Rb1Lds L;
+    if ((int)blockIdx.x < nb64)
+        rb1_body<FL, 64, true, false>(L, blockIdx.x, g64, rc, X, Y, rhs, st, partials, counter,
+                                      it, nullptr, 0, 0, nullptr, nullptr, neu);
+    else
+        rb1_body<FL, TC2, true, false>(L, blockIdx.x - nb64, g2, rc, X, Y, rhs, st, partials,
+                                       counter, it, nullptr, 0, 0, nullptr, nullptr, neu);
 }
 
 // R (the first colour SOR-updated, linear_solver_redblack.c:97-114) of a

@@ -543,6 +543,18 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                           c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
                           c->counter, it, (const double*)nullptr, 0, 0, (Mbox*)nullptr,        \
                           (unsigned long long*)nullptr, neu_fold ? 1 : 0)
+            if (c->rb_strip_tc && rb1_pf) {
+                // full-width tiles and the narrow strip in one grid
+                const SGeo& gm = c->rg_main;
+                const SGeo& gs = c->rg_strip;
+                const int nbm = gm.tiles_x * gm.tiles_y * gm.tiles_z;
+                const unsigned nbt = (unsigned)(nbm + gs.tiles_x * gs.tiles_y * gs.tiles_z);
+                timed(c, HIP_KT_RELAX, [&] {
+                    hipExtLaunchKernelGGL((k_rb1m<FL, 16>), dim3(nbt), dim3(1024), 0, c->stream,
+                                          c->ta, c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs,
+                                          c->rxst, c->partials, c->counter, it, neu_fold ? 1 : 0);
+                }, it);
+            } else
             timed(c, HIP_KT_RELAX, [&] {
                 if (!rb1_pf) RB1_LAUNCH(64, false);
                 else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
@@ -945,6 +957,39 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         rg.kc = std::max(1, std::min(rg.kc, nint_k));
         rg.tiles_z = (nint_k + rg.kc - 1) / rg.kc;
         n_partials = std::max(n_partials, rg.tiles_x * rg.tiles_y * rg.tiles_z);
+        // the last x tile of a TC-64 launch is partial unless 124 divides the
+        // row: its workgroups run a full tile's steps for a few columns
+        // (512^3: 14 of 124). Up to 28 such columns run instead as a strip
+        // of TC-16 tiles (28 columns x 60 rows, 4.8x fewer workgroups) in
+        // the same grid (k_rb1m). CFD_HIP_RB1_STRIP=0: off.
+        const char* estrip = getenv("CFD_HIP_RB1_STRIP");
+        c->rb_strip_tc = 0;
+        if (tc == 64 && c->nranks == 1 && !(estrip && atoi(estrip) == 0)) {
+            const int T = (int)(nx / 124), R = (int)nx - 124 * T;
+            // TC-32 strips (R in 29..60) measured slower (1024^2 x 512: 2.96 vs
+            // 2.93 ms); TC-16 ones faster (512^3: 0.734 vs 0.760 ms,
+            // profiles/r03_rb1_strip.jsonl)
+            const int stc = (R == 0) ? 0 : (R <= 28 ? 16 : 0);
+            if (stc) {
+                c->rb_strip_tc = stc;
+                SGeo& m = c->rg_main;
+                SGeo& q = c->rg_strip;
+                m = rg;
+                m.tiles_x = T;
+                q = rg;
+                q.xofs = 124 * T;
+                q.tiles_x = 1;
+                const int oy = 1024 / stc - 4;
+                q.tiles_y = (int)((ny - 1 + oy - 1) / oy);
+                q.kc = std::max(1, std::min(rg.kc, nint_k));
+                q.tiles_z = (nint_k + q.kc - 1) / q.kc;
+                // one grid (k_rb1m): partial slot = blockIdx.x, total = gridDim.x
+                m.part_ofs = q.part_ofs = 0;
+                m.part_total = q.part_total = 0;
+                n_partials = std::max(n_partials, m.tiles_x * m.tiles_y * m.tiles_z +
+                                                      q.tiles_x * q.tiles_y * q.tiles_z);
+            }
+        }
         // Z-slabs: output planes k0+1 .. k1-2 split into two halves around
         // the edge planes (relax_solve_fused); CFD_HIP_RB_SPLIT=0 keeps the
         // one-launch iteration with blocking exchanges (A/B)

@@ -12,5 +12,5 @@ tail -3 $O/pytest_gpu.log
 for f in 1 0; do
   CFD_HIP_RB1_FOLD=$f timeout -k 10 200 python3 bench.py --case convection --size 1024 --steps 1 --warmup 0 \
       > $O/conv_fold$f.json 2> $O/conv_fold$f.err || { echo "conv fold=$f failed"; tail -5 $O/conv_fold$f.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('$O/conv_fold$f.json')); print('fold=$f', d['ms_per_step'], d['rbsor_iters_per_step'], d['rbsor_iter_ms'], d['roofline']['avg_launch_ms'])"
+  python3 -c "import json,sys; d=json.load(open('$O/conv_fold$f.json')); print('fold=$f', d['ms_per_step'], d['rbsor_iters_per_step'], d['rbsor_iter_ms'], d['roofline']['avg_sweep_ms'])"
 done
