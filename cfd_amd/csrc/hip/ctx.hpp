@@ -124,8 +124,6 @@ struct hip_proj_ctx {
     double* rho = nullptr;  // per-cell density (RK4 reads rho[idx]); lazily allocated
     double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3
     double *dxa = nullptr, *dya = nullptr;  // grid->dx[], grid->dy[] (RK4 per-index spacing)
-    double *rdx = nullptr, *rdy = nullptr;  // RN(1/(2 d)), RN(1/d^2) per index, interleaved
-    std::vector<double> h_rdx, h_rdy;
     double *src_u_row = nullptr, *src_v_col = nullptr;
     std::vector<double> h_src_u, h_src_v;
     // reductions / state

@@ -1593,16 +1593,6 @@ __device__ __forceinline__ void rk_rhs(const RkCoef& rc, const RkNbr& n, double 
     }
 }
 
-// a / d correctly rounded, like divc, for operands that are often exactly
-// zero (derivatives of a field at rest): e = q d - a and q - e r give the
-// signed zero of a / d for a = +-0, so zeros stay on the fast path.
-__device__ __forceinline__ double divz(double a, double d, double r) {
-    const double q = a * r;
-    const double aq = fabs(q);
-    if (!(aq <= 0x1p+900 && (aq >= 0x1p-900 || aq == 0.0))) return a / d;
-    return fma(-fma(q, d, -a), r, q);
-}
-
 template <int STAGE, bool BUOY>
 __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
                                                   Fld4 out, const double* __restrict__ rho,
@@ -1666,21 +1656,14 @@ __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fl
 // nx - 2 by address), y / z neighbours are pair loads of the (periodically
 // resolved) neighbour row / plane. Half the load instructions of k_rk_stage;
 // rk_rhs is shared, so the values are bitwise the per-cell kernel's.
-// r03: the differences' divisions by the per-index spacings (2 dx_i, dx_i^2,
-// 2 dy_j, dy_j^2; solver_rk4.c via ns_momentum_rhs_scalar.h) go through divz
-// with host-computed correctly rounded reciprocals (rdx[2i] = RN(1/(2 dx_i)),
-// rdx[2i+1] = RN(1/dx_i^2), rdy likewise): bitwise the reference's `/`, three
-// VALU ops instead of the generic fp64 division (16 per cell).
 template <int STAGE, bool BUOY>
-__global__ __launch_bounds__(256, 4) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
+__global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
                                                    Fld4 out, const double* __restrict__ rho,
                                                    const double* __restrict__ T,
                                                    const double* __restrict__ dxa,
                                                    const double* __restrict__ dya,
                                                    const double* __restrict__ su_row,
-                                                   const double* __restrict__ sv_col,
-                                                   const double* __restrict__ rdx,
-                                                   const double* __restrict__ rdy) {
+                                                   const double* __restrict__ sv_col) {
     const int i0 = blockIdx.x * 128 + 2 * (threadIdx.x & 63);
     const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int k = blockIdx.z;
@@ -1708,8 +1691,6 @@ __global__ __launch_bounds__(256, 4) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur
         const double2 t2 = BUOY ? ld2(T, idx) : make_double2(0.0, 0.0);
         const double dyj = dya[j], su = su_row[j];
         const double dxa0 = dxa[i0], dxa1 = dxa[min(i0 + 1, g.nx - 1)];
-        const double2 rxa = ld2(rdx, 2LL * i0), rxb = ld2(rdx, 2LL * min(i0 + 1, g.nx - 1));
-        const double2 ry = ld2(rdy, 2LL * j);
         const bool oka = ina && !(r2.x <= 1e-10) && !(fabs(dxa0) < 1e-10) && !(fabs(dyj) < 1e-10);
         const bool okb = inb && !(r2.y <= 1e-10) && !(fabs(dxa1) < 1e-10) && !(fabs(dyj) < 1e-10);
         const double2 uc = ld2(cur.f[0], idx), vc = ld2(cur.f[1], idx), wc = ld2(cur.f[2], idx);
@@ -1724,17 +1705,17 @@ __global__ __launch_bounds__(256, 4) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur
             const double bl = (i0 + 1 > 1) ? c2.x : F[row + (g.nx - 2)];
             const double tdxa = 2.0 * dxa0, tdxb = 2.0 * dxa1, tdy = 2.0 * dyj;
             const double dxxa = dxa0 * dxa0, dxxb = dxa1 * dxa1, dyy = dyj * dyj;
-            da.dx = divz(ar - xl, tdxa, rxa.x);
-            da.dy = divz(u2.x - d2.x, tdy, ry.x);
+            da.dx = (ar - xl) / tdxa;
+            da.dy = (u2.x - d2.x) / tdy;
             da.dz = (p2.x - m2.x) * rc.inv_2dz;
-            da.xx = divz(ar - 2.0 * c2.x + xl, dxxa, rxa.y);
-            da.yy = divz(u2.x - 2.0 * c2.x + d2.x, dyy, ry.y);
+            da.xx = (ar - 2.0 * c2.x + xl) / dxxa;
+            da.yy = (u2.x - 2.0 * c2.x + d2.x) / dyy;
             da.zz = (p2.x - 2.0 * c2.x + m2.x) * rc.inv_dz2;
-            db.dx = divz(xr - bl, tdxb, rxb.x);
-            db.dy = divz(u2.y - d2.y, tdy, ry.x);
+            db.dx = (xr - bl) / tdxb;
+            db.dy = (u2.y - d2.y) / tdy;
             db.dz = (p2.y - m2.y) * rc.inv_2dz;
-            db.xx = divz(xr - 2.0 * c2.y + bl, dxxb, rxb.y);
-            db.yy = divz(u2.y - 2.0 * c2.y + d2.y, dyy, ry.y);
+            db.xx = (xr - 2.0 * c2.y + bl) / dxxb;
+            db.yy = (u2.y - 2.0 * c2.y + d2.y) / dyy;
             db.zz = (p2.y - 2.0 * c2.y + m2.y) * rc.inv_dz2;
         };
         D1 pa_, pb_;
@@ -2697,6 +2678,15 @@ static __global__ __launch_bounds__(256) void k_rb_edge_r(SGeo g, RelaxCoef rc,
 #endif
 constexpr int PR_TY = CFD_PR_TY;  // rows (waves) per workgroup
 
+// a / d correctly rounded, like divc, for operands that are often exactly
+// zero (derivatives of a field at rest): e = q d - a and q - e r give the
+// signed zero of a / d for a = +-0, so zeros stay on the fast path.
+__device__ __forceinline__ double divz(double a, double d, double r) {
+    const double q = a * r;
+    const double aq = fabs(q);
+    if (!(aq <= 0x1p+900 && (aq >= 0x1p-900 || aq == 0.0))) return a / d;
+    return fma(-fma(q, d, -a), r, q);
+}
 // divz with the range test deferred into a lane flag (see DivC)
 struct DivFastZ {
     bool& ok;

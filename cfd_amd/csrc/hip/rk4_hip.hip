@@ -17,8 +17,6 @@ static cfd_status_t ensure_rk(hip_proj_ctx* c) {
     if (!c->xt) ST_TRY(dalloc(c, &c->xt, n));
     if (!c->dxa) ST_TRY(dalloc(c, &c->dxa, c->nx));
     if (!c->dya) ST_TRY(dalloc(c, &c->dya, c->ny));
-    if (!c->rdx) ST_TRY(dalloc(c, &c->rdx, 2 * c->nx));
-    if (!c->rdy) ST_TRY(dalloc(c, &c->rdy, 2 * c->ny));
     if (!c->rho) {
         // no per-cell density supplied: uniform rho0 (what set_density sets)
         ST_TRY(dalloc(c, &c->rho, n));
@@ -46,11 +44,11 @@ static void launch_stage(hip_proj_ctx* c, bool buoy, const RkCoef& rc, const Fld
         if (buoy)
             hipExtLaunchKernelGGL((k_rk_stage2<S, true>), g2, dim3(256), 0, c->stream, c->ta,
                                   c->tb, 0, c->geo, rc, cur, q0, acc, out, c->rho, c->T, c->dxa,
-                                  c->dya, c->src_u_row, c->src_v_col, c->rdx, c->rdy);
+                                  c->dya, c->src_u_row, c->src_v_col);
         else
             hipExtLaunchKernelGGL((k_rk_stage2<S, false>), g2, dim3(256), 0, c->stream, c->ta,
                                   c->tb, 0, c->geo, rc, cur, q0, acc, out, c->rho, c->T, c->dxa,
-                                  c->dya, c->src_u_row, c->src_v_col, c->rdx, c->rdy);
+                                  c->dya, c->src_u_row, c->src_v_col);
         return;
     }
     const dim3 grid = cell_grid(c);
@@ -87,21 +85,6 @@ static cfd_status_t rk4_step_impl(hip_proj_ctx* c, const grid* g, const ns_solve
     // evaluated on the host with the reference's libm expressions
     HIP_TRY(hipMemcpyAsync(c->dxa, g->dx, nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->dya, g->dy, ny * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    // correctly rounded reciprocals of the stage kernel's divisors (divz)
-    c->h_rdx.resize(2 * nx);
-    c->h_rdy.resize(2 * ny);
-    for (size_t i = 0; i < nx; i++) {
-        c->h_rdx[2 * i] = 1.0 / (2.0 * g->dx[i]);
-        c->h_rdx[2 * i + 1] = 1.0 / (g->dx[i] * g->dx[i]);
-    }
-    for (size_t j = 0; j < ny; j++) {
-        c->h_rdy[2 * j] = 1.0 / (2.0 * g->dy[j]);
-        c->h_rdy[2 * j + 1] = 1.0 / (g->dy[j] * g->dy[j]);
-    }
-    HIP_TRY(hipMemcpyAsync(c->rdx, c->h_rdx.data(), 2 * nx * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->rdy, c->h_rdy.data(), 2 * ny * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
     c->h_src_u.resize(ny);
     c->h_src_v.resize(nx);
     for (size_t j = 0; j < ny; j++)
