@@ -71,9 +71,6 @@ struct hip_proj_ctx {
     // second launch sharing the residual reduction (rb_strip_tc 0: none)
     SGeo rg_main{}, rg_strip{};
     int rb_strip_tc = 0;
-    // one device: two RB-SOR iterations per sweep (k_rb2, 120 x 8 tiles)
-    SGeo rgeo2{};
-    int rb2 = 0;
     int rb1_tc = 64;           // k_rb1 tile width in x pairs (64, 32, 16)
     SGeo pgeo{};               // predictor / corrector z-march tiling (k_pred2, k_corr2)
     int split_b = 0;
@@ -97,7 +94,6 @@ struct hip_proj_ctx {
     double *r = nullptr, *pa = nullptr, *pb = nullptr;  // r; CG search directions
     double *pc4 = nullptr, *pd4 = nullptr;               // (ring of CG_XFOLD = 4: pa pb pc4 pd4)
     double *rhs = nullptr, *xt = nullptr;
-    double* xt2 = nullptr;  // third relaxation buffer of the two-iteration sweep (k_rb2)
     // RK4 borrows r, p_a, p_b, x_tmp as stage buffers and leaves wall values in
     // them; the CG needs zero wall cells in r and the p ring (lagged-BC
     // semantics), so the next CG solve clears them first.

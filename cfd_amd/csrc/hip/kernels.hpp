@@ -2625,311 +2625,6 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1m(
                                        counter, it, nullptr, 0, 0, nullptr, nullptr, neu);
 }
 
-// ---------------------------------------------------------------------------
-// Two RB-SOR iterations per sweep (r03, one device, 3-D, Neumann BC): X -> Y1
-// -> Y2 in one z-march, so an iteration reads X and rhs and writes its
-// iterate once per TWO iterations' worth of row loads. Step q forms
-//   S1  R1_{q+1}: first colour of X (linear_solver_redblack.c:97-114)
-//   S2  Y1_q:     second colour from R1 (:116-133)  -> stored (the result
-//                 when the solve stops after the first iteration of the pair)
-//   S3  R2_{q-1}: first colour of Y1
-//   S4  Y2_{q-2}: second colour from R2              -> stored
-// with the L-inf residuals of X (S1) and of Y1 (S3) alongside
-// (linear_solver.c:304-346). Between the two iterations the reference applies
-// the Neumann BC (:139): every boundary cell of Y1 becomes its inward
-// neighbour, so wherever iteration 2 (S3, S4 and the residual of Y1) reads a
-// boundary cell it reads the cell whose stencil it computes instead (the face
-// value IS that cell's value; edges and corners are no interior cell's
-// neighbours). Stores fold the Neumann shell as k_rb1 does.
-// Tile: 128 x 16 cells loaded, the validity shrinking one cell per stage, so
-// 120 x 8 are written (lanes 2..61, rows 4..11). LDS: X, R1, Y1, R2 rows by
-// plane parity (128 KB), one barrier per step. Every per-cell expression and
-// operand is the reference's, so Y1, Y2 and both residuals are bitwise.
-// The last workgroup applies the common loop's decision for the iterates after
-// s and after s + 1 iterations (s = the pair's first sweep index) and leaves
-// in RxState.result the decided iterate's index mod 3 (the three buffers the
-// host rotates: X = buf[s % 3], Y1 = buf[(s + 1) % 3], Y2 = buf[(s + 2) % 3]).
-// ---------------------------------------------------------------------------
-struct Rb2Lds {
-    double xb[2][16][2][64];
-    double r1b[2][16][2][64];
-    double y1b[2][16][2][64];
-    double r2b[2][16][2][64];
-    double sh[2][16];
-    int flag;
-};
-
-template <int FL>
-static __global__ __launch_bounds__(1024, 4) void k_rb2(
-    SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y1,
-    double* __restrict__ Y2, const double* __restrict__ rhs, RxState* st, double* partials,
-    unsigned* counter, int s0) {
-    constexpr int NW = 16, TR = 16, OX = 120, OY = 8;
-    __shared__ Rb2Lds L;
-    auto lget = [&](double (&a)[2][16][2][64], int p, int r, int l) __attribute__((always_inline)) {
-        return make_double2(a[p][r][0][l], a[p][r][1][l]);
-    };
-    auto lput = [&](double (&a)[2][16][2][64], int p, int r, int l, double2 v)
-                    __attribute__((always_inline)) {
-        a[p][r][0][l] = v.x;
-        a[p][r][1][l] = v.y;
-    };
-    if (st->done) return;
-    const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
-    const int t = xcd_tile(blockIdx.x, nt);
-    const int tx = t % g.tiles_x;
-    const int rest = t / g.tiles_x;
-    const int ty = rest % g.tiles_y;
-    const int tz = rest / g.tiles_y;
-    const int lane = threadIdx.x & 63;
-    const int r = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // tile row = wave
-    const int c = lane;
-    const int cm = max(c - 1, 0), cp = min(c + 1, 63);
-    const int rlo = max(r - 1, 0), rhi = min(r + 1, TR - 1);
-    const int i0 = tx * OX - 4 + 2 * c;
-    const int j = ty * OY - 4 + r;  // wave-uniform
-    const int kb = g.k0 + tz * g.kc;
-    const int ke = min(kb + g.kc, g.k1);
-    const bool jin = (j >= 1 && j <= g.ny - 2);
-    const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;
-    const bool in1 = jin && i0 + 1 >= 1 && i0 + 1 <= g.nx - 2;
-    const bool ownl = (c >= 2 && c <= 61);
-    const bool doR1 = (r >= 1 && r <= 14), doY1 = (r >= 2 && r <= 13);
-    const bool doR2 = (r >= 3 && r <= 12), doY2 = (r >= 4 && r <= 11);
-    const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
-    const int ic = (i0 < g.nx) ? max(i0, 0) : g.nx - 2 - ((g.nx - 2) & 1);
-    const int jr = j + (r == 0 ? 1 : (r == TR - 1 ? -1 : 0));
-    const long long colx = (long long)max(min(j, g.ny - 1), 0) * g.px + ic;
-    const long long colr = (long long)max(min(jr, g.ny - 1), 0) * g.px + ic;
-    auto ldx = [&](int k) -> double2 {
-        return ld2(X, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx);
-    };
-    auto ldr = [&](int k) -> double2 {
-        return ld2v<FL>(rhs, (long long)min(max(k, 0), g.nz - 1) * g.ps + colr);
-    };
-    // own cells (lanes 2..61 of rows 4..11 inside the grid's x/y range); the
-    // boundary shell of Y1 / Y2 is written by k_rx_shell (Neumann) after the
-    // sweep, on Y2 every pair and on Y1 when the solve ends on it
-    const bool st_ok = ownl && doY2 && jin && i0 < g.nx;
-    double* __restrict__ const Y1c = Y1 + col;
-    double* __restrict__ const Y2c = Y2 + col;
-    const double2 zero = make_double2(0.0, 0.0);
-    const int q0 = kb - 4;
-    double2 xr[4], br[2];
-    xr[0] = ldx(q0);
-    xr[1] = ldx(q0 + 1);
-    xr[2] = ldx(q0 + 2);
-    xr[3] = zero;
-    br[0] = ldr(q0 + 1);
-    br[1] = zero;
-    double2 rm1 = zero, y1m = zero, y1c = zero, r2m = zero, b0 = zero, b1 = zero;
-    double rmm1h = 0.0, r2mmh = 0.0, b2h = 0.0;
-    lput(L.xb, 1, r, c, xr[1]);  // X_{q0+1}: phase 0 reads buffer (0 + 1) & 1
-    double m0 = 0.0, m1 = 0.0;
-    auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
-        constexpr bool E = decltype(Ec)::value;
-        constexpr int P = decltype(Pc)::value;
-        constexpr int IM = P & 3, IC = (P + 1) & 3, IP = (P + 2) & 3, IN = (P + 3) & 3;
-        constexpr int BQ = P & 1, BN = (P + 1) & 1;
-        xr[IN] = ldx(q + 3);
-        br[BN] = ldr(q + 2);
-        const double2 xm = xr[IM], xc = xr[IC], xp = xr[IP], bq = br[BQ];
-        __syncthreads();
-        // LDS operands, read stage by stage (only the component a one-cell
-        // update needs) to bound the live registers
-        // LDS buffers alternate with the step; indexed by the compile-time phase P
-        // (same alternation as the plane parity, immediate LDS offsets)
-        constexpr int pX = (P + 1) & 1, pR1 = P & 1, pY1 = (P + 1) & 1, pR2 = P & 1;
-        constexpr int EC = E ? 0 : 1;  // the component this step's updates touch
-        const double2 ys = lget(L.xb, pX, rlo, c), yn = lget(L.xb, pX, rhi, c);
-        const double left = L.xb[pX][r][1][cm], right = L.xb[pX][r][0][cp];
-        // ---- S1: R1_{q+1} (+ residual of X_{q+1}) ----
-        const int qa = q + 1;
-        double2 R = xc;
-        if (doR1 && qa >= g.k0 && qa < g.k1) {
-            if (E) {
-                const double v = sor1(rc, DivC{}, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
-                if (in0) R.x = v;
-            } else {
-                const double v = sor1(rc, DivC{}, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
-                if (in1) R.y = v;
-            }
-            if (doY2 && qa >= kb && qa < ke && ownl) {
-                const double a0 = res1(rc, DivC{}, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);
-                const double a1 = res1(rc, DivC{}, xc.y, xc.x, right, ys.y, yn.y, xm.y, xp.y, bq.y);
-                if (in0 && a0 > m0) m0 = a0;
-                if (in1 && a1 > m0) m0 = a1;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the stages' live ranges apart
-        // ---- S2: Y1_q (second colour of plane q from R1) ----
-        double2 o1 = rm1;
-        if (doY1 && q >= g.k0 && q < g.k1) {
-            const double rys = L.r1b[pR1][rlo][EC][c], ryn = L.r1b[pR1][rhi][EC][c];
-            const double rlr = E ? L.r1b[pR1][r][1][cm] : L.r1b[pR1][r][0][cp];
-            if (E) {
-                const double v = sor1(rc, DivC{}, rm1.x, rlr, rm1.y, rys, ryn, rmm1h, R.x, b0.x);
-                if (in0) o1.x = v;
-            } else {
-                const double v = sor1(rc, DivC{}, rm1.y, rm1.x, rlr, rys, ryn, rmm1h, R.y, b0.y);
-                if (in1) o1.y = v;
-            }
-        }
-        // the Neumann BC between the iterations, on Y1's x faces in the
-        // registers: (0) <- (1), (nx-1) <- (nx-2) (inside the pair, or from
-        // the lane to the left when nx is odd); the y faces are the rows the
-        // row-1 / row-(ny-2) waves also publish, the z faces are read as the
-        // centre (S3, S4)
-        if (i0 == 0) o1.x = o1.y;
-        if (i0 + 1 == g.nx - 1) o1.y = o1.x;
-        {
-            const double up = __shfl_up(o1.y, 1, 64);
-            if (i0 == g.nx - 1) o1.x = up;
-        }
-        if (st_ok && q >= kb && q < ke) st2v<FL>(Y1c, (long long)q * g.ps, o1);
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- S3: R2_{q-1} (first colour of Y1) + residual of Y1_{q-1} ----
-        const int qc = q - 1;
-        double2 R2 = y1c;
-        if (doR2 && qc >= g.k0 && qc < g.k1) {
-            const double2 y1s = lget(L.y1b, pY1, rlo, c), y1n = lget(L.y1b, pY1, rhi, c);
-            const double y1l = L.y1b[pY1][r][1][cm], y1r = L.y1b[pY1][r][0][cp];
-            // z faces: plane 0 / nz-1 of Y1 is plane 1 / nz-2 (wave-uniform)
-            const double2 zm = (qc == 1) ? y1c : y1m;
-            const double2 zp = (qc == g.nz - 2) ? y1c : o1;
-            if (E) {
-                const double v = sor1(rc, DivC{}, y1c.x, y1l, y1c.y, y1s.x, y1n.x, zm.x, zp.x, b1.x);
-                if (in0) R2.x = v;
-            } else {
-                const double v = sor1(rc, DivC{}, y1c.y, y1c.x, y1r, y1s.y, y1n.y, zm.y, zp.y, b1.y);
-                if (in1) R2.y = v;
-            }
-            if (doY2 && qc >= kb && qc < ke && ownl) {
-                const double a0 = res1(rc, DivC{}, y1c.x, y1l, y1c.y, y1s.x, y1n.x, zm.x, zp.x, b1.x);
-                const double a1 = res1(rc, DivC{}, y1c.y, y1c.x, y1r, y1s.y, y1n.y, zm.y, zp.y, b1.y);
-                if (in0 && a0 > m1) m1 = a0;
-                if (in1 && a1 > m1) m1 = a1;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- S4: Y2_{q-2} (second colour from R2) ----
-        const int qd = q - 2;
-        double2 o2 = r2m;
-        if (doY2 && qd >= g.k0 && qd < g.k1) {
-            const double r2s = L.r2b[pR2][rlo][EC][c], r2n = L.r2b[pR2][rhi][EC][c];
-            const double r2lr = E ? L.r2b[pR2][r][1][cm] : L.r2b[pR2][r][0][cp];
-            const double zm = (qd == 1) ? (E ? r2m.x : r2m.y) : r2mmh;
-            const double zp = (qd == g.nz - 2) ? (E ? r2m.x : r2m.y) : (E ? R2.x : R2.y);
-            if (E) {
-                const double v = sor1(rc, DivC{}, r2m.x, r2lr, r2m.y, r2s, r2n, zm, zp, b2h);
-                if (in0) o2.x = v;
-            } else {
-                const double v = sor1(rc, DivC{}, r2m.y, r2m.x, r2lr, r2s, r2n, zm, zp, b2h);
-                if (in1) o2.y = v;
-            }
-        }
-        if (st_ok && qd >= kb && qd < ke) st2v<FL>(Y2c, (long long)qd * g.ps, o2);
-        // ---- shift to step q + 1 (which updates the other component) ----
-        rmm1h = E ? rm1.y : rm1.x;
-        rm1 = R;
-        y1m = y1c;
-        y1c = o1;
-        r2mmh = E ? r2m.y : r2m.x;
-        r2m = R2;
-        b2h = E ? b1.y : b1.x;
-        b1 = b0;
-        b0 = bq;
-        lput(L.xb, P & 1, r, c, xp);
-        lput(L.r1b, (P + 1) & 1, r, c, R);
-        // Y1 and R2 rows for iteration 2: rows j = 0 / ny-1 (the y faces) hold
-        // the copies rows 1 / ny-2 publish, not their own values
-        if (j != 0 && j != g.ny - 1) {
-            lput(L.y1b, P & 1, r, c, o1);
-            lput(L.r2b, (P + 1) & 1, r, c, R2);
-        }
-        if (j == 1 && r > 0) {
-            lput(L.y1b, P & 1, r - 1, c, o1);
-            lput(L.r2b, (P + 1) & 1, r - 1, c, R2);
-        }
-        if (j == g.ny - 2 && r < TR - 1) {
-            lput(L.y1b, P & 1, r + 1, c, o1);
-            lput(L.r2b, (P + 1) & 1, r + 1, c, R2);
-        }
-    };
-    // E(q) for the row: ((j + q + kofs) & 1) == 0; wave-uniform
-    const bool E0 = ((j + q0 + g.kofs) & 1) == 0;
-    int q = q0;
-    const int qend = ke + 2;  // last step q = ke + 1 writes Y2_{ke-1}
-    auto march = [&](auto E0c) __attribute__((always_inline)) {
-        constexpr bool A = decltype(E0c)::value;
-        using TA = BoolC<A>;
-        using TB = BoolC<!A>;
-        for (; q + 3 < qend; q += 4) {
-            step(TA{}, IntC<0>{}, q);
-            step(TB{}, IntC<1>{}, q + 1);
-            step(TA{}, IntC<2>{}, q + 2);
-            step(TB{}, IntC<3>{}, q + 3);
-        }
-        if (q < qend) step(TA{}, IntC<0>{}, q);
-        if (q + 1 < qend) step(TB{}, IntC<1>{}, q + 1);
-        if (q + 2 < qend) step(TA{}, IntC<2>{}, q + 2);
-    };
-    if (E0) march(BoolC<true>{});
-    else march(BoolC<false>{});
-    // ---- the two residual maxima: partials[2 b], [2 b + 1]; last workgroup decides ----
-    m0 = wave_max(m0);
-    m1 = wave_max(m1);
-    if (lane == 0) {
-        L.sh[0][r] = m0;
-        L.sh[1][r] = m1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = 0.0, b = 0.0;
-        for (int v = 0; v < NW; ++v) {
-            a = fmax(a, L.sh[0][v]);
-            b = fmax(b, L.sh[1][v]);
-        }
-        store_sc1(&partials[2 * blockIdx.x], a);
-        store_sc1(&partials[2 * blockIdx.x + 1], b);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned tk = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        L.flag = (tk == gridDim.x - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (L.flag == 0) return;
-    double a = 0.0, b = 0.0;
-    for (unsigned blk = threadIdx.x; blk < gridDim.x; blk += 1024) {
-        a = fmax(a, load_sc1(&partials[2 * blk]));
-        b = fmax(b, load_sc1(&partials[2 * blk + 1]));
-    }
-    a = wave_max(a);
-    b = wave_max(b);
-    if (lane == 0) {
-        L.sh[0][r] = a;
-        L.sh[1][r] = b;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t0 = 0.0, t1 = 0.0;
-        for (int v = 0; v < NW; ++v) {
-            t0 = fmax(t0, L.sh[0][v]);
-            t1 = fmax(t1, L.sh[1][v]);
-        }
-        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rx_finish(st, t0, s0);
-        int dec = s0;
-        if (!st->done && s0 + 1 <= st->max_iter) {
-            rx_finish(st, t1, s0 + 1);
-            dec = s0 + 1;
-        }
-        // the decided iterate's buffer (dec % 3), + 3 when it is a Y1 (dec odd:
-        // its boundary shell is written by the host's Neumann launch)
-        if (st->done) st->result = dec % 3 + 3 * (dec & 1);
-    }
-}
-
 // R (the first colour SOR-updated, linear_solver_redblack.c:97-114) of a
 // slab's two edge planes k0 and k1 - 1 into RH, for the neighbours' k_rb1
 // (DIST); same operands and order as k_rb1's R, so bitwise equal to it.

@@ -586,61 +586,6 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
         }
         return CFD_SUCCESS;
     };
-    // two iterations per sweep (k_rb2): sweeps s = 0, 2, 4, ...; the iterate
-    // after s iterations lives in B[s % 3]
-    const bool pair = single && !D && neu_fold && c->rb2;
-    if (pair) {
-        if (!c->xt2) ST_TRY(dalloc(c, &c->xt2, field_elems(c)));
-        double* B[3] = {c->pn, c->xt, c->xt2};
-        const unsigned nb2 =
-            (unsigned)(c->rgeo2.tiles_x * c->rgeo2.tiles_y * c->rgeo2.tiles_z);
-        RxState* hs2 = reinterpret_cast<RxState*>(c->h_state);
-        int s = 0, chunk = 4, slot = 0, prev = -1;
-        const int chunk_max = std::max(1, c->cfg.poll_interval / 2);
-        while (s <= max_iter) {
-            for (int q = 0; q < chunk && s <= max_iter; ++q, s += 2) {
-                timed(c, HIP_KT_RELAX, [&] {
-                    hipExtLaunchKernelGGL((k_rb2<FL>), dim3(nb2), dim3(1024), 0, c->stream, c->ta,
-                                          c->tb, 0, c->rgeo2, rc, B[s % 3], B[(s + 1) % 3],
-                                          B[(s + 2) % 3], c->rhs, c->rxst, c->partials,
-                                          c->counter, s);
-                }, s);
-                // Y2's Neumann shell (the next pair's X), unless the solve stopped
-                hipExtLaunchKernelGGL(k_rx_shell, dim3(shell_blocks(c)), dim3(256), 0, c->stream,
-                                      c->ta, c->tb, 0, c->geo, c->rxst, B[(s + 2) % 3],
-                                      B[(s + 2) % 3], 1);
-            }
-            HIP_TRY(hipMemcpyAsync(&hs2[slot], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost,
-                                   c->stream));
-            HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
-            if (prev >= 0) {
-                HIP_TRY(hipEventSynchronize(c->ev_poll[prev]));
-                if (hs2[prev].done) break;
-            }
-            prev = slot;
-            slot ^= 1;
-            chunk = std::min(chunk * 2, chunk_max);
-        }
-        HIP_TRY(hipMemcpyAsync(&hs2[2], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost,
-                               c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        flush_timing(c);
-        const RxState& r = hs2[2];
-        if (!r.done) {
-            set_err(CFD_ERROR, "relaxation: device loop ended without a decision");
-            return CFD_ERROR;
-        }
-        const int k = r.result % 3;  // the decided iterate's buffer
-        if (r.result >= 3) launch_bc(c, B[k], 0, DirVals{});  // a Y1: its Neumann shell
-        c->pn = B[k];
-        c->xt = B[(k + 1) % 3];
-        c->xt2 = B[(k + 2) % 3];
-        c->pstats.initial_residual = r.res0;
-        c->pstats.iterations = r.iterations;
-        c->pstats.final_residual = r.res;
-        c->pstats.status = (poisson_solver_status_t)r.status;
-        return (r.status == ST_CONVERGED) ? CFD_SUCCESS : CFD_ERROR_MAX_ITER;
-    }
     // iterations 0..max_iter: sweep it also yields the residual after it - 1
     // iterations, so the last launch only completes the final test
     RxState* hs = reinterpret_cast<RxState*>(c->h_state);  // pinned, >= 3 RxState
@@ -1074,26 +1019,6 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             c->rg_in2.part_ofs = n1 + ne;
             c->rg_in1.part_total = c->rg_edge.part_total = c->rg_in2.part_total = n1 + ne + n2;
             n_partials = std::max(n_partials, n1 + ne + n2);
-        }
-    }
-    {   // two-iteration RB-SOR sweep (k_rb2): 120 x 8 written per 128 x 16 loaded,
-        // one device, 3-D; CFD_HIP_RB2=0 keeps one iteration per sweep
-        const char* e2 = getenv("CFD_HIP_RB2");
-        c->rb2 = (c->nranks == 1 && nz > 1 && nint_k >= 1 && !(e2 && atoi(e2) == 0)) ? 1 : 0;
-        if (c->rb2) {
-            SGeo& q = c->rgeo2;
-            q = sg;
-            q.kmode = 0;
-            q.part_ofs = q.part_total = 0;
-            q.tiles_x = (int)((nx - 1 + 119) / 120);
-            q.tiles_y = (int)((ny - 1 + 7) / 8);
-            q.kc = 128;  // a z run costs a six-plane prologue
-            while (q.kc > 16 &&
-                   (long long)q.tiles_x * q.tiles_y * ((nint_k + q.kc - 1) / q.kc) < 1024)
-                q.kc /= 2;
-            q.kc = std::max(1, std::min(q.kc, nint_k));
-            q.tiles_z = (nint_k + q.kc - 1) / q.kc;
-            n_partials = std::max(n_partials, q.tiles_x * q.tiles_y * q.tiles_z);
         }
     }
     {   // predictor / corrector: 128 x PR_TY x kc tiles, >= ~8 workgroups per CU
