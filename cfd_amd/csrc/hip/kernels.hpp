@@ -3053,6 +3053,233 @@ static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
     corr_reduce(mv, mp, bad, red);
 }
 
+// ---------------------------------------------------------------------------
+// r03: the predictor and corrector on the CG sweeps' 128 x 16 tiles with the
+// y neighbours from LDS (k_pred3, k_corr3). Each wave owns one row of the
+// tile, the two edge waves also load the row beyond it (the y halo), and
+// every wave publishes its centre row once per plane: a stencil field's rows
+// are read from HBM 18 times per 16 rows written, where the 4-row tiles of
+// k_pred2 / k_corr2 need L2 hits for 6 reads per 4 rows (k_pred2 fetched
+// 45.8 B/cell for 24 B of reads, profiles/r02e_rocprof_summary.txt). One
+// barrier per plane, rows double-buffered by plane parity. Operands and
+// operation order are k_pred2's / k_corr2's, so the results are bitwise
+// theirs. FL: SW_NT_STORE = non-temporal stores of the outputs, SW_NT_LOAD =
+// non-temporal loads of the pointwise inputs (the corrector's u*, v*, w*).
+// ---------------------------------------------------------------------------
+constexpr int PC_TY = 16;
+
+template <bool BUOY, int FL>
+static __global__ __launch_bounds__(64 * PC_TY, 1) void k_pred3(
+    SGeo g, PredCoef2 pc, const double* __restrict__ U, const double* __restrict__ V,
+    const double* __restrict__ W, const double* __restrict__ T,
+    const double* __restrict__ src_u_row, const double* __restrict__ src_v_col,
+    double* __restrict__ us, double* __restrict__ vs, double* __restrict__ ws) {
+    constexpr int TY = PC_TY;
+    __shared__ double2 rows[2][3][TY + 2][64];
+    const RowPair c = row_pair<TY>(g);
+    const bool halo = (c.w == 0) || (c.w == TY - 1);
+    const int jc = min(c.j, g.ny - 1);
+    const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
+    const int hslot = (c.w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - jc) * g.px;
+    const bool xok = c.i0 < g.nx;
+    const bool eok = (c.lane == 0 && c.i0 >= 1 && xok) || (c.lane == 63 && c.i0 + 2 < g.nx);
+    const long long eoff = (c.lane == 0) ? -1 : 2;
+    const double su = src_u_row[jc];
+    const double sv0 = xok ? src_v_col[c.i0] : 0.0;
+    const double sv1 = c.in1 ? src_v_col[c.i0 + 1] : 0.0;
+    const double* F[3] = {U, V, W};
+    double* O[3] = {us, vs, ws};
+    const double2 zero = make_double2(0.0, 0.0);
+    long long idx = c.idx;
+    // rows of plane k are published into rows[k & 1] at the end of step
+    // k - 1 (that buffer was last read in step k - 2, before the barrier of
+    // step k - 1), so no row value is held in registers across a barrier
+    double2 pm[3], pcv[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        pm[f] = ld2(F[f], idx - g.sz);
+        pcv[f] = ld2(F[f], idx);
+        rows[0][f][c.w + 1][c.lane] = pcv[f];
+        if (halo) rows[0][f][hslot][c.lane] = ld2(F[f], idx + hoff);
+    }
+    int buf = 0;
+    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        // this plane's loads: the z+ centre row, the halo row of plane k + 1,
+        // the x-edge cells, T
+        double2 pp[3], hn[3];
+        double e[3];
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            pp[f] = ld2(F[f], idx + g.sz);
+            hn[f] = halo ? ld2(F[f], idx + g.sz + hoff) : zero;
+            e[f] = eok ? F[f][idx + eoff] : 0.0;
+        }
+        const double2 tc = BUOY ? ld2(T, idx) : zero;
+        __syncthreads();
+        const double u0 = pcv[0].x, u1 = pcv[0].y;
+        const double v0 = pcv[1].x, v1 = pcv[1].y;
+        const double w0 = pcv[2].x, w1 = pcv[2].y;
+        double s0[3] = {su, sv0, 0.0}, s1[3] = {su, sv1, 0.0};
+        if (BUOY) {
+            const double dT0 = tc.x - pc.T_ref, dT1 = tc.y - pc.T_ref;
+            s0[0] += -pc.beta * dT0 * pc.g0;
+            s0[1] += -pc.beta * dT0 * pc.g1;
+            s0[2] += -pc.beta * dT0 * pc.g2;
+            s1[0] += -pc.beta * dT1 * pc.g0;
+            s1[1] += -pc.beta * dT1 * pc.g1;
+            s1[2] += -pc.beta * dT1 * pc.g2;
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            const double2 ys = rows[buf][f][c.w][c.lane];
+            const double2 yn = rows[buf][f][c.w + 2][c.lane];
+            const double l = __shfl_up(pcv[f].y, 1, 64);
+            const double rr = __shfl_down(pcv[f].x, 1, 64);
+            const double left = c.lane == 0 ? e[f] : l;
+            const double right = c.lane == 63 ? e[f] : rr;
+            double r0, r1;
+            auto compute = [&](auto dv) __attribute__((always_inline)) {
+                r0 = pred_cell(pc, dv, u0, v0, w0, pcv[f].x, left, pcv[f].y, ys.x, yn.x, pm[f].x,
+                               pp[f].x, s0[f]);
+                r1 = pred_cell(pc, dv, u1, v1, w1, pcv[f].y, pcv[f].x, right, ys.y, yn.y, pm[f].y,
+                               pp[f].y, s1[f]);
+            };
+            bool ok = true;
+            compute(DivFastZ{ok});
+            if (__builtin_expect(wave_any_bad(ok), 0)) {
+                if (!ok) compute(DivExact{});
+            }
+            double2 o = pcv[f];  // boundary cells: u* = u
+            if (c.in0) o.x = r0;
+            if (c.in1) o.y = r1;
+            if (c.act) st2v<FL>(O[f], idx, o);
+        }
+        buf ^= 1;
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            pm[f] = pcv[f];
+            pcv[f] = pp[f];
+            rows[buf][f][c.w + 1][c.lane] = pp[f];
+            if (halo) rows[buf][f][hslot][c.lane] = hn[f];
+        }
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ void corr_reduce_n(double mv, double mp, bool bad,
+                                              unsigned long long* red) {
+    __shared__ double shv[NW], shp[NW];
+    __shared__ int shbad;
+    if (threadIdx.x == 0) shbad = 0;
+    __syncthreads();
+    mv = wave_max(mv);
+    mp = wave_max(mp);
+    if (bad) shbad = 1;
+    if ((threadIdx.x & 63) == 0) {
+        shv[threadIdx.x >> 6] = mv;
+        shp[threadIdx.x >> 6] = mp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = shv[0], b = shp[0];
+        for (int q = 1; q < NW; ++q) {
+            a = fmax(a, shv[q]);
+            b = fmax(b, shp[q]);
+        }
+        atomicMax(&red[0], ord_enc(a));
+        atomicMax(&red[1], ord_enc(b));
+        if (shbad) atomicOr(&red[2], 1ull);
+    }
+}
+
+template <int FL>
+static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
+    SGeo g, CorrCoef2 cc, const double* __restrict__ us, const double* __restrict__ vs,
+    const double* __restrict__ ws, const double* __restrict__ P, double* __restrict__ U,
+    double* __restrict__ V, double* __restrict__ W, unsigned long long* red) {
+    constexpr int TY = PC_TY;
+    __shared__ double2 rows[2][TY + 2][64];
+    const RowPair c = row_pair<TY>(g);
+    const bool halo = (c.w == 0) || (c.w == TY - 1);
+    const int jc = min(c.j, g.ny - 1);
+    const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
+    const int hslot = (c.w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - jc) * g.px;
+    const bool xok = c.i0 < g.nx;
+    const bool eok = (c.lane == 0 && c.i0 >= 1 && xok) || (c.lane == 63 && c.i0 + 2 < g.nx);
+    const long long eoff = (c.lane == 0) ? -1 : 2;
+    const double2 zero = make_double2(0.0, 0.0);
+    double mv = 0.0, mp = 0.0;
+    bool bad = false;
+    long long idx = c.idx;
+    double2 pm = ld2(P, idx - g.sz), pcv = ld2(P, idx);
+    rows[0][c.w + 1][c.lane] = pcv;  // publishing as in k_pred3
+    if (halo) rows[0][hslot][c.lane] = ld2(P, idx + hoff);
+    int buf = 0;
+    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        const double2 pp = ld2(P, idx + g.sz);
+        const double2 hn = halo ? ld2(P, idx + g.sz + hoff) : zero;
+        const double e = eok ? P[idx + eoff] : 0.0;
+        const double2 qa = ld2v<FL>(us, idx), qb = ld2v<FL>(vs, idx), qc = ld2v<FL>(ws, idx);
+        __syncthreads();
+        const double2 ys = rows[buf][c.w][c.lane];
+        const double2 yn = rows[buf][c.w + 2][c.lane];
+        const double l = __shfl_up(pcv.y, 1, 64);
+        const double rr = __shfl_down(pcv.x, 1, 64);
+        const double left = c.lane == 0 ? e : l;
+        const double right = c.lane == 63 ? e : rr;
+        double2 nu = qa, nv = qb, nw = qc;  // boundary cells: u = u* (== u)
+        double dx0, dy0, dx1, dy1;
+        auto compute = [&](auto dv) __attribute__((always_inline)) {
+            dx0 = dv(pcv.y - left, cc.two_dx, cc.r_two_dx);
+            dy0 = dv(yn.x - ys.x, cc.two_dy, cc.r_two_dy);
+            dx1 = dv(right - pcv.x, cc.two_dx, cc.r_two_dx);
+            dy1 = dv(yn.y - ys.y, cc.two_dy, cc.r_two_dy);
+        };
+        bool ok = true;
+        compute(DivFastZ{ok});
+        if (__builtin_expect(wave_any_bad(ok), 0)) {
+            if (!ok) compute(DivExact{});
+        }
+        {
+            const double dp_dz = (pp.x - pm.x) * cc.inv_2dz;
+            const double x0 = fmax(-100.0, fmin(100.0, qa.x - cc.dt_over_rho * dx0));
+            const double y0 = fmax(-100.0, fmin(100.0, qb.x - cc.dt_over_rho * dy0));
+            const double w0 = fmax(-100.0, fmin(100.0, qc.x - cc.dt_over_rho * dp_dz));
+            if (c.in0) {
+                nu.x = x0;
+                nv.x = y0;
+                nw.x = w0;
+            }
+        }
+        {
+            const double dp_dz = (pp.y - pm.y) * cc.inv_2dz;
+            const double x1 = fmax(-100.0, fmin(100.0, qa.y - cc.dt_over_rho * dx1));
+            const double y1 = fmax(-100.0, fmin(100.0, qb.y - cc.dt_over_rho * dy1));
+            const double w1 = fmax(-100.0, fmin(100.0, qc.y - cc.dt_over_rho * dp_dz));
+            if (c.in1) {
+                nu.y = x1;
+                nv.y = y1;
+                nw.y = w1;
+            }
+        }
+        if (c.act) {
+            st2v<FL>(U, idx, nu);
+            st2v<FL>(V, idx, nv);
+            st2v<FL>(W, idx, nw);
+            cell_stats(nu.x, nv.x, nw.x, pcv.x, mv, mp, bad);
+            if (c.i0 + 1 < g.nx) cell_stats(nu.y, nv.y, nw.y, pcv.y, mv, mp, bad);
+        }
+        pm = pcv;
+        pcv = pp;
+        buf ^= 1;
+        rows[buf][c.w + 1][c.lane] = pp;
+        if (halo) rows[buf][hslot][c.lane] = hn;
+    }
+    corr_reduce_n<TY>(mv, mp, bad, red);
+}
+
 // Stats over the boundary shell cells the corrector's z-march does not visit
 // (rows j = 0, ny - 1 of the owned planes, the global z faces): u, v, w are
 // the caller's boundary values there. Planes [ks, ke) as in the corrector.

@@ -1031,6 +1031,25 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         const long long zt = std::max(1LL, (4LL * c->grid_cap / PR_TY + xy - 1) / xy);
         pg.kc = (int)std::max<long long>(1, (nint_k + zt - 1) / zt);
         pg.tiles_z = (nint_k + pg.kc - 1) / pg.kc;
+        // k_pred3 / k_corr3: the CG sweeps' 128 x 16 tiles, long z runs
+        // shortened until every CU has a workgroup (one 1024-thread
+        // workgroup per CU: 110 KB of LDS)
+        SGeo& p3 = c->pgeo16;
+        p3 = sg;
+        p3.kmode = 0;
+        p3.tiles_x = (int)((nx + 127) / 128);
+        p3.tiles_y = (int)((ny + PC_TY - 1) / PC_TY);
+        p3.kc = 256;
+        while (p3.kc > 4 && (long long)p3.tiles_x * p3.tiles_y * ((nint_k + p3.kc - 1) / p3.kc) <
+                                c->grid_cap / 8)
+            p3.kc /= 2;
+        p3.kc = std::max(1, std::min(p3.kc, nint_k));
+        p3.tiles_z = (nint_k + p3.kc - 1) / p3.kc;
+        c->pc3 = 0;
+        if (const char* e = getenv("CFD_HIP_PC3")) {  // A/B: k_pred3 / k_corr3 (ctx.hpp)
+            const int v = atoi(e);
+            c->pc3 = (v == 1 || v == 2 || v == 4) ? v : 0;
+        }
     }
     c->split_b = (c->nranks > 1 && nint_k >= 3) ? 1 : 0;
     if (c->split_b) {
@@ -1485,10 +1504,26 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     // slabs: the neighbours' planes of everything the stencils read
     ST_TRY(halo(c, {c->u, c->v, c->w, c->p}));
     if (buoy || energy) ST_TRY(halo(c, {c->T}));
+    const unsigned np3 =
+        (unsigned)(c->pgeo16.tiles_x * c->pgeo16.tiles_y * c->pgeo16.tiles_z);
     timed(c, HIP_KT_PREDICTOR, [&] {
         // PF = 0: one plane's loads per step (the plane-ahead schedule
         // measured slower, profiles/r02_step_kernels.jsonl)
-        if (buoy)
+        auto p3 = [&](auto kern) {
+            hipExtLaunchKernelGGL(kern, dim3(np3), dim3(64 * PC_TY), 0, c->stream, c->ta, c->tb, 0,
+                                  c->pgeo16, pc, c->u, c->v, c->w, c->T, c->src_u_row,
+                                  c->src_v_col, c->us, c->vs, c->ws);
+        };
+        if (c->pc3 == 1) {
+            if (buoy) p3(k_pred3<true, 0>);
+            else p3(k_pred3<false, 0>);
+        } else if (c->pc3 == 2) {
+            if (buoy) p3(k_pred3<true, SW_NT_STORE>);
+            else p3(k_pred3<false, SW_NT_STORE>);
+        } else if (c->pc3 == 4) {
+            if (buoy) p3(k_pred3<true, SW_NT_STORE | SW_NT_LOAD>);
+            else p3(k_pred3<false, SW_NT_STORE | SW_NT_LOAD>);
+        } else if (buoy)
             hipExtLaunchKernelGGL((k_pred2<true, 0>), dim3(npg), dim3(64 * PR_TY), 0, c->stream,
                                   c->ta, c->tb, 0, c->pgeo, pc, c->u, c->v, c->w, c->T,
                                   c->src_u_row, c->src_v_col, c->us, c->vs, c->ws);
@@ -1550,9 +1585,18 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     cc.dt_over_rho = dt / rho;
     hipExtLaunchKernelGGL(k_init_red, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->red);
     timed(c, HIP_KT_CORRECTOR, [&] {
-        hipExtLaunchKernelGGL((k_corr2<0>), dim3(npg), dim3(64 * PR_TY), 0, c->stream, c->ta,
-                              c->tb, 0, c->pgeo, cc, c->us, c->vs, c->ws, c->pn, c->u, c->v, c->w,
-                              c->red);
+        auto c3 = [&](auto kern) {
+            hipExtLaunchKernelGGL(kern, dim3(np3), dim3(64 * PC_TY), 0, c->stream, c->ta, c->tb, 0,
+                                  c->pgeo16, cc, c->us, c->vs, c->ws, c->pn, c->u, c->v, c->w,
+                                  c->red);
+        };
+        if (c->pc3 == 1) c3(k_corr3<0>);
+        else if (c->pc3 == 2) c3(k_corr3<SW_NT_STORE>);
+        else if (c->pc3 == 4) c3(k_corr3<SW_NT_STORE | SW_NT_LOAD>);
+        else
+            hipExtLaunchKernelGGL((k_corr2<0>), dim3(npg), dim3(64 * PR_TY), 0, c->stream, c->ta,
+                                  c->tb, 0, c->pgeo, cc, c->us, c->vs, c->ws, c->pn, c->u, c->v,
+                                  c->w, c->red);
     });
     hipExtLaunchKernelGGL(k_shell_stats, dim3(shell_blocks(c)), dim3(256), 0, c->stream, c->ta,
                           c->tb, 0, c->geo, c->u, c->v, c->w, c->pn, c->red);
