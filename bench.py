@@ -534,7 +534,11 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
 
 
 # timer -> kernel symbol in the PMC profile (the CG sweeps are named per variant)
-TIMER_KERNEL = {"predictor": "k_pred2<false, 0>", "corrector": "k_corr2<0>",
+# (predictor / corrector: k_pred3 / k_corr3 by default, k_pred2 / k_corr2 with
+# CFD_HIP_PC3=0; FL 0 is the product variant)
+_PC_OLD = os.environ.get("CFD_HIP_PC3", "1") == "0"
+TIMER_KERNEL = {"predictor": "k_pred2<false, 0>" if _PC_OLD else "k_pred3<false, 0>",
+                "corrector": "k_corr2<0>" if _PC_OLD else "k_corr3<0>",
                 "cg_setup": "k_cg_setup<true, false, true, false>"}
 
 

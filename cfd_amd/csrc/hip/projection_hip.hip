@@ -1045,7 +1045,10 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             p3.kc /= 2;
         p3.kc = std::max(1, std::min(p3.kc, nint_k));
         p3.tiles_z = (nint_k + p3.kc - 1) / p3.kc;
-        c->pc3 = 0;
+        // default k_pred3 / k_corr3 (r03: predictor 1.47 -> 1.25 ms, fetch
+        // 45.7 -> 25.6 B/cell at 512^3, profiles/r03_pc3.jsonl);
+        // CFD_HIP_PC3=0 selects k_pred2 / k_corr2
+        c->pc3 = 1;
         if (const char* e = getenv("CFD_HIP_PC3")) {  // A/B: k_pred3 / k_corr3 (ctx.hpp)
             const int v = atoi(e);
             c->pc3 = (v == 1 || v == 2 || v == 4) ? v : 0;
