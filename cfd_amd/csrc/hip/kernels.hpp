@@ -625,8 +625,29 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     }
     Bundle cur;
     if (PF) cur = issue(c.kb, idx);
+    // (r03) the prologue's loads land before the march: otherwise the
+    // compiler's wait for a prologue register merges, at the loop's compute
+    // block, with the pending prefetch of the next plane into one vmcnt(0),
+    // i.e. every step waited for plane k + 1 before computing plane k (a
+    // builtin, not inline asm: the waitcnt pass sees only real waits; the
+    // empty asm keeps the prologue's loads above it)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+        // p of plane k is known here: store it before the next plane's loads
+        // are issued (r03). Stored after them, the compiler's in-order vmcnt
+        // wait for the store (its source registers are reused by the step's
+        // arithmetic) also waited for the whole prefetch bundle, so plane
+        // k + 1's loads landed before plane k was computed. (FOLD reads the
+        // old p_{it-4} of plane k from pn in the bundle: its store stays after
+        // the step.)
+        if (!FOLD && c.act) {
+            double2 pw;
+            pw.x = c.in0 ? pc.x : 0.0;
+            pw.y = c.in1 ? pc.y : 0.0;
+            st2v<FL>(pn, idx, pw);
+        }
         Bundle nxt;
         if (PF) {
             if (k + 1 < c.ke) nxt = issue(k + 1, idx + g.ps);
@@ -655,7 +676,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
                          : cur.fxo.y;
             st2v<FL>(fx, idx, xw);
         }
-        if (c.act) {
+        if (FOLD && c.act) {
             double2 pw;
             pw.x = c.in0 ? pc.x : 0.0;
             pw.y = c.in1 ? pc.y : 0.0;
@@ -1650,12 +1671,119 @@ __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fl
     }
 }
 
+// First and second differences of one field at the cells (i0, i0 + 1) of a
+// pair (r02b, shared by k_rk_stage2 / k_rk_stage3): c2 the pair, d2 / u2 the
+// (periodically resolved) y- / y+ rows, m2 / p2 the z- / z+ planes, xl the
+// left of i0, ar the right of i0, bl the left of i0 + 1, xr the right of
+// i0 + 1. Same expressions and order as rk_rhs, so the values are bitwise.
+struct RkD1 {
+    double dx, dy, dz, xx, yy, zz;
+};
+
+__device__ __forceinline__ void rk_pair_diffs(const RkCoef& rc, double2 c2, double2 d2, double2 u2,
+                                              double2 m2, double2 p2, double xl, double ar,
+                                              double bl, double xr, double dxa0, double dxa1,
+                                              double dyj, RkD1& da, RkD1& db) {
+    const double tdxa = 2.0 * dxa0, tdxb = 2.0 * dxa1, tdy = 2.0 * dyj;
+    const double dxxa = dxa0 * dxa0, dxxb = dxa1 * dxa1, dyy = dyj * dyj;
+    da.dx = (ar - xl) / tdxa;
+    da.dy = (u2.x - d2.x) / tdy;
+    da.dz = (p2.x - m2.x) * rc.inv_2dz;
+    da.xx = (ar - 2.0 * c2.x + xl) / dxxa;
+    da.yy = (u2.x - 2.0 * c2.x + d2.x) / dyy;
+    da.zz = (p2.x - 2.0 * c2.x + m2.x) * rc.inv_dz2;
+    db.dx = (xr - bl) / tdxb;
+    db.dy = (u2.y - d2.y) / tdy;
+    db.dz = (p2.y - m2.y) * rc.inv_2dz;
+    db.xx = (xr - 2.0 * c2.y + bl) / dxxb;
+    db.yy = (u2.y - 2.0 * c2.y + d2.y) / dyy;
+    db.zz = (p2.y - 2.0 * c2.y + m2.y) * rc.inv_dz2;
+}
+
+// The stage derivatives of a pair (rk_rhs's expressions): diffs(f, da, db)
+// yields field f's differences; p first (its gradient enters u, v, w), then
+// u, v, w, so only one field's neighbourhood is live at a time.
+template <bool BUOY, class Diffs>
+__device__ __forceinline__ void rk_pair_kr(const RkCoef& rc, Diffs diffs, double2 uc, double2 vc,
+                                           double2 wc, double2 r2, double2 t2, double su,
+                                           double sv0, double sv1, bool oka, bool okb,
+                                           double (&kra)[4], double (&krb)[4]) {
+    RkD1 pa_, pb_;
+    diffs(3, pa_, pb_);
+    const double dpxa = clampl(pa_.dx, 100.0), dpya = clampl(pa_.dy, 100.0),
+                 dpza = clampl(pa_.dz, 100.0);
+    const double dpxb = clampl(pb_.dx, 100.0), dpyb = clampl(pb_.dy, 100.0),
+                 dpzb = clampl(pb_.dz, 100.0);
+    const double nua = fmin(rc.mu / fmax(r2.x, 1e-10), 1.0);
+    const double nub = fmin(rc.mu / fmax(r2.y, 1e-10), 1.0);
+    double sa[3] = {su, sv0, 0.0};
+    double sb[3] = {su, sv1, 0.0};
+    if (BUOY) {
+        const double dTa = t2.x - rc.T_ref, dTb = t2.y - rc.T_ref;
+        sa[0] += -rc.beta * dTa * rc.g0;
+        sa[1] += -rc.beta * dTa * rc.g1;
+        sa[2] += -rc.beta * dTa * rc.g2;
+        sb[0] += -rc.beta * dTb * rc.g0;
+        sb[1] += -rc.beta * dTb * rc.g1;
+        sb[2] += -rc.beta * dTb * rc.g2;
+    }
+    const double gpa[3] = {dpxa, dpya, dpza}, gpb[3] = {dpxb, dpyb, dpzb};
+    double diva = 0.0, divb = 0.0;  // du_dx + dv_dy + dw_dz (clamped terms)
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        RkD1 da, db;
+        diffs(f, da, db);
+        da.dx = clampl(da.dx, 100.0); da.dy = clampl(da.dy, 100.0); da.dz = clampl(da.dz, 100.0);
+        db.dx = clampl(db.dx, 100.0); db.dy = clampl(db.dy, 100.0); db.dz = clampl(db.dz, 100.0);
+        da.xx = clampl(da.xx, 1000.0); da.yy = clampl(da.yy, 1000.0); da.zz = clampl(da.zz, 1000.0);
+        db.xx = clampl(db.xx, 1000.0); db.yy = clampl(db.yy, 1000.0); db.zz = clampl(db.zz, 1000.0);
+        if (oka)
+            kra[f] = -uc.x * da.dx - vc.x * da.dy - wc.x * da.dz - gpa[f] / r2.x +
+                     nua * (da.xx + da.yy + da.zz) + sa[f];
+        if (okb)
+            krb[f] = -uc.y * db.dx - vc.y * db.dy - wc.y * db.dz - gpb[f] / r2.y +
+                     nub * (db.xx + db.yy + db.zz) + sb[f];
+        const double ta = (f == 0) ? da.dx : (f == 1 ? da.dy : da.dz);
+        const double tb = (f == 0) ? db.dx : (f == 1 ? db.dy : db.dz);
+        diva = (f == 0) ? ta : diva + ta;
+        divb = (f == 0) ? tb : divb + tb;
+    }
+    if (oka) kra[3] = -0.1 * r2.x * fmax(-10.0, fmin(10.0, diva));
+    if (okb) krb[3] = -0.1 * r2.y * fmax(-10.0, fmin(10.0, divb));
+}
+
+// The stage update of one pair of field q (solver_rk4.c stage sums): stage
+// 0 stores k into the running sum, 1-2 add 2k, 3 forms the final state.
+template <int STAGE, int FL = 0>
+__device__ __forceinline__ void rk_pair_update(const RkCoef& rc, const Fld4& q0, const Fld4& acc,
+                                               const Fld4& out, int q, long long idx, double ka,
+                                               double kb) {
+    const double2 q02 = ld2v<FL>(q0.f[q], idx);
+    double2 o;
+    if (STAGE == 0) {
+        st2v<FL>(acc.f[q], idx, make_double2(ka, kb));
+        o = make_double2(q02.x + rc.fac * ka, q02.y + rc.fac * kb);
+    } else if (STAGE < 3) {
+        const double2 a2 = ld2v<FL>(acc.f[q], idx);
+        st2v<FL>(acc.f[q], idx, make_double2(a2.x + 2.0 * ka, a2.y + 2.0 * kb));
+        o = make_double2(q02.x + rc.fac * ka, q02.y + rc.fac * kb);
+    } else {
+        const double2 a2 = ld2v<FL>(acc.f[q], idx);
+        o = make_double2(q02.x + rc.fac * (a2.x + ka), q02.y + rc.fac * (a2.y + kb));
+    }
+    if (q < 3) {
+        o.x = fmax(-100.0, fmin(100.0, o.x));
+        o.y = fmax(-100.0, fmin(100.0, o.y));
+    }
+    st2v<FL>(out.f[q], idx, o);
+}
+
 // The same stage on x pairs (r02b): each lane owns cells (i0, i0 + 1) and
 // moves every field with 16-B loads / stores; the cell's x neighbours are the
 // pair's other cell or one scalar load (the periodic indices of i = 1 and
 // nx - 2 by address), y / z neighbours are pair loads of the (periodically
 // resolved) neighbour row / plane. Half the load instructions of k_rk_stage;
-// rk_rhs is shared, so the values are bitwise the per-cell kernel's.
+// rk_rhs's expressions, so the values are bitwise the per-cell kernel's.
 template <int STAGE, bool BUOY>
 __global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, Fld4 q0, Fld4 acc,
                                                    Fld4 out, const double* __restrict__ rho,
@@ -1685,8 +1813,6 @@ __global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, F
         // x neighbours outside the pair: left of i0, right of i0 + 1
         const long long la = (i0 > 1) ? idx - 1 : row + (g.nx - 2);
         const long long rb = (i0 + 1 < g.nx - 2) ? idx + 2 : row + 1;
-        // one field at a time (p first: its gradient enters u, v, w), so only
-        // one field's neighbourhood is live: same expressions as rk_rhs
         const double2 r2 = ld2(rho, idx);
         const double2 t2 = BUOY ? ld2(T, idx) : make_double2(0.0, 0.0);
         const double dyj = dya[j], su = su_row[j];
@@ -1694,93 +1820,156 @@ __global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, F
         const bool oka = ina && !(r2.x <= 1e-10) && !(fabs(dxa0) < 1e-10) && !(fabs(dyj) < 1e-10);
         const bool okb = inb && !(r2.y <= 1e-10) && !(fabs(dxa1) < 1e-10) && !(fabs(dyj) < 1e-10);
         const double2 uc = ld2(cur.f[0], idx), vc = ld2(cur.f[1], idx), wc = ld2(cur.f[2], idx);
-        struct D1 { double dx, dy, dz, xx, yy, zz; };
-        // first and second differences of field f at both cells
-        auto diffs = [&](int f, D1& da, D1& db) __attribute__((always_inline)) {
+        auto diffs = [&](int f, RkD1& da, RkD1& db) __attribute__((always_inline)) {
             const double* F = cur.f[f];
             const double2 c2 = ld2(F, idx), d2 = ld2(F, jd), u2 = ld2(F, ju);
             const double2 m2 = ld2(F, kd), p2 = ld2(F, ku);
             const double xl = F[la], xr = F[rb];
             const double ar = (i0 < g.nx - 2) ? c2.y : F[row + 1];
             const double bl = (i0 + 1 > 1) ? c2.x : F[row + (g.nx - 2)];
-            const double tdxa = 2.0 * dxa0, tdxb = 2.0 * dxa1, tdy = 2.0 * dyj;
-            const double dxxa = dxa0 * dxa0, dxxb = dxa1 * dxa1, dyy = dyj * dyj;
-            da.dx = (ar - xl) / tdxa;
-            da.dy = (u2.x - d2.x) / tdy;
-            da.dz = (p2.x - m2.x) * rc.inv_2dz;
-            da.xx = (ar - 2.0 * c2.x + xl) / dxxa;
-            da.yy = (u2.x - 2.0 * c2.x + d2.x) / dyy;
-            da.zz = (p2.x - 2.0 * c2.x + m2.x) * rc.inv_dz2;
-            db.dx = (xr - bl) / tdxb;
-            db.dy = (u2.y - d2.y) / tdy;
-            db.dz = (p2.y - m2.y) * rc.inv_2dz;
-            db.xx = (xr - 2.0 * c2.y + bl) / dxxb;
-            db.yy = (u2.y - 2.0 * c2.y + d2.y) / dyy;
-            db.zz = (p2.y - 2.0 * c2.y + m2.y) * rc.inv_dz2;
+            rk_pair_diffs(rc, c2, d2, u2, m2, p2, xl, ar, bl, xr, dxa0, dxa1, dyj, da, db);
         };
-        D1 pa_, pb_;
-        diffs(3, pa_, pb_);
-        const double dpxa = clampl(pa_.dx, 100.0), dpya = clampl(pa_.dy, 100.0),
-                     dpza = clampl(pa_.dz, 100.0);
-        const double dpxb = clampl(pb_.dx, 100.0), dpyb = clampl(pb_.dy, 100.0),
-                     dpzb = clampl(pb_.dz, 100.0);
-        const double nua = fmin(rc.mu / fmax(r2.x, 1e-10), 1.0);
-        const double nub = fmin(rc.mu / fmax(r2.y, 1e-10), 1.0);
-        double sa[3] = {su, sv_col[i0], 0.0};
-        double sb[3] = {su, sv_col[min(i0 + 1, g.nx - 1)], 0.0};
-        if (BUOY) {
-            const double dTa = t2.x - rc.T_ref, dTb = t2.y - rc.T_ref;
-            sa[0] += -rc.beta * dTa * rc.g0;
-            sa[1] += -rc.beta * dTa * rc.g1;
-            sa[2] += -rc.beta * dTa * rc.g2;
-            sb[0] += -rc.beta * dTb * rc.g0;
-            sb[1] += -rc.beta * dTb * rc.g1;
-            sb[2] += -rc.beta * dTb * rc.g2;
-        }
-        const double gpa[3] = {dpxa, dpya, dpza}, gpb[3] = {dpxb, dpyb, dpzb};
-        double diva = 0.0, divb = 0.0;  // du_dx + dv_dy + dw_dz (clamped terms)
-#pragma unroll
-        for (int f = 0; f < 3; ++f) {
-            D1 da, db;
-            diffs(f, da, db);
-            da.dx = clampl(da.dx, 100.0); da.dy = clampl(da.dy, 100.0); da.dz = clampl(da.dz, 100.0);
-            db.dx = clampl(db.dx, 100.0); db.dy = clampl(db.dy, 100.0); db.dz = clampl(db.dz, 100.0);
-            da.xx = clampl(da.xx, 1000.0); da.yy = clampl(da.yy, 1000.0); da.zz = clampl(da.zz, 1000.0);
-            db.xx = clampl(db.xx, 1000.0); db.yy = clampl(db.yy, 1000.0); db.zz = clampl(db.zz, 1000.0);
-            if (oka)
-                kra[f] = -uc.x * da.dx - vc.x * da.dy - wc.x * da.dz - gpa[f] / r2.x +
-                         nua * (da.xx + da.yy + da.zz) + sa[f];
-            if (okb)
-                krb[f] = -uc.y * db.dx - vc.y * db.dy - wc.y * db.dz - gpb[f] / r2.y +
-                         nub * (db.xx + db.yy + db.zz) + sb[f];
-            const double ta = (f == 0) ? da.dx : (f == 1 ? da.dy : da.dz);
-            const double tb = (f == 0) ? db.dx : (f == 1 ? db.dy : db.dz);
-            diva = (f == 0) ? ta : diva + ta;
-            divb = (f == 0) ? tb : divb + tb;
-        }
-        if (oka) kra[3] = -0.1 * r2.x * fmax(-10.0, fmin(10.0, diva));
-        if (okb) krb[3] = -0.1 * r2.y * fmax(-10.0, fmin(10.0, divb));
+        rk_pair_kr<BUOY>(rc, diffs, uc, vc, wc, r2, t2, su, sv_col[i0],
+                         sv_col[min(i0 + 1, g.nx - 1)], oka, okb, kra, krb);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const double2 q02 = ld2(q0.f[q], idx);
-        double2 o;
-        if (STAGE == 0) {
-            st2(acc.f[q], idx, make_double2(kra[q], krb[q]));
-            o = make_double2(q02.x + rc.fac * kra[q], q02.y + rc.fac * krb[q]);
-        } else if (STAGE < 3) {
-            const double2 a2 = ld2(acc.f[q], idx);
-            st2(acc.f[q], idx, make_double2(a2.x + 2.0 * kra[q], a2.y + 2.0 * krb[q]));
-            o = make_double2(q02.x + rc.fac * kra[q], q02.y + rc.fac * krb[q]);
-        } else {
-            const double2 a2 = ld2(acc.f[q], idx);
-            o = make_double2(q02.x + rc.fac * (a2.x + kra[q]), q02.y + rc.fac * (a2.y + krb[q]));
+    for (int q = 0; q < 4; ++q) rk_pair_update<STAGE>(rc, q0, acc, out, q, idx, kra[q], krb[q]);
+}
+
+// r03: the stage as a z-march over 128 x TY tiles with the y neighbours of
+// the four stencil fields from LDS (k_pred3's scheme): each wave owns one row,
+// the two edge waves also load the rows beyond the tile, every wave publishes
+// its centre row once per plane (rows double-buffered by plane parity, one
+// barrier per plane), and the z neighbours are a register ring, so u, v, w, p
+// are read from HBM once per stage instead of up to three times (k_rk_stage2
+// takes y / z neighbours from the caches). The march covers every plane of
+// the grid (the boundary planes take the pointwise update only). Periodic
+// neighbours (ns_momentum_rhs_scalar.h via solver_rk4.c): rows 1 / ny - 2 take
+// the wrapped row by a direct load, the ring takes plane nz - 2 as the z-
+// neighbour of plane 1 and plane nz - 2's z+ load is plane 1; x wraps and the
+// tile's x edges are one scalar load per side and field. Operands and order are
+// k_rk_stage2's (rk_pair_diffs / rk_pair_kr / rk_pair_update): bitwise. 3-D
+// grids (nz >= 3) on one device.
+template <int STAGE, bool BUOY, int TY>
+__global__ __launch_bounds__(64 * TY, 1) void k_rk_stage3(SGeo g, RkCoef rc, Fld4 cur, Fld4 q0,
+                                                         Fld4 acc, Fld4 out,
+                                                         const double* __restrict__ rho,
+                                                         const double* __restrict__ T,
+                                                         const double* __restrict__ dxa,
+                                                         const double* __restrict__ dya,
+                                                         const double* __restrict__ su_row,
+                                                         const double* __restrict__ sv_col) {
+    __shared__ double2 rows[2][4][TY + 2][64];
+    const RowPair c = row_pair<TY>(g);
+    const int lane = c.lane, w = c.w, i0 = c.i0, j = c.j;
+    const int nx = g.nx, ny = g.ny, nz = g.nz;
+    const bool halo = (w == 0) || (w == TY - 1);
+    const int jc = min(j, ny - 1);
+    const int jh = (w == 0) ? max(j - 1, 0) : min(j + 1, ny - 1);
+    const int hslot = (w == 0) ? 0 : TY + 1;
+    const long long hoff = (long long)(jh - jc) * g.px;
+    const bool valid = (i0 < nx) && (j < ny);   // the pair's cells are stored
+    const bool yin = (j >= 1 && j <= ny - 2);   // row j has interior cells
+    const bool ina0 = yin && i0 >= 1 && i0 <= nx - 2;
+    const bool inb0 = yin && i0 + 1 <= nx - 2;
+    // wrapped y rows: row 1 takes row ny - 2 as y-, row ny - 2 takes row 1 as
+    // y+ (one row holds both when ny == 3); wave-uniform
+    const bool yw = yin && (j == 1 || j == ny - 2);
+    const long long ywoff = (long long)((j == 1 ? ny - 2 : 1) - jc) * g.px;
+    // x neighbours outside the lane's pair: eL (lane 0: cell i0 - 1, or
+    // nx - 2 for i0 == 0), eR (cell 1 where the pair wraps: i0 == nx - 2 or
+    // i0 + 1 == nx - 2; else lane 63: cell i0 + 2)
+    const long long rowst = (long long)jc * g.px;  // row start in plane 0
+    const bool needL = valid && lane == 0 && (i0 == 0 || i0 >= 2);
+    const long long offL = (i0 == 0) ? (long long)(nx - 2) : (long long)(i0 - 1);
+    const bool wrapR = (i0 == nx - 2) || (i0 + 1 == nx - 2);
+    const bool needR = valid && (wrapR || (lane == 63 && i0 + 2 < nx));
+    const long long offR = wrapR ? 1LL : (long long)(i0 + 2);
+    const double dyj = dya[jc], su = su_row[jc];
+    const double dxa0 = i0 < nx ? dxa[i0] : 0.0, dxa1 = dxa[min(i0 + 1, nx - 1)];
+    const double sv0 = i0 < nx ? sv_col[i0] : 0.0, sv1 = sv_col[min(i0 + 1, nx - 1)];
+    const double2 zero = make_double2(0.0, 0.0);
+    auto plane = [&](int k) -> long long { return (long long)min(max(k, 0), nz - 1) * g.ps; };
+    const long long cofs = c.idx - c.kb * g.ps;  // the pair in plane 0
+    // LDS holds plane k's rows (centre and y halo) in rows[k & 1] and, in the
+    // centre slots of rows[(k & 1) ^ 1], plane k's z- neighbour (plane k - 1;
+    // plane nz - 2 for plane 1): a thread reads back only its own centre
+    // slot of the z- plane, which it alone rewrites (with plane k + 1) after
+    // the step, so only the y neighbours need the barrier. Registers carry
+    // just the loads of plane k + 1 (plane 1 at the step of plane nz - 2: the
+    // wrapped z+), so the march has no register ring.
+    {
+        const long long om = plane(c.kb == 1 ? nz - 2 : c.kb - 1);
+        const long long oc = plane(c.kb);
+        const int b0 = c.kb & 1;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            rows[b0 ^ 1][f][w + 1][lane] = ld2(cur.f[f], om + cofs);
+            rows[b0][f][w + 1][lane] = ld2(cur.f[f], oc + cofs);
+            if (halo) rows[b0][f][hslot][lane] = ld2(cur.f[f], oc + cofs + hoff);
         }
-        if (q < 3) {
-            o.x = fmax(-100.0, fmin(100.0, o.x));
-            o.y = fmax(-100.0, fmin(100.0, o.y));
+    }
+    for (int k = c.kb; k < c.ke; ++k) {
+        const long long oc = plane(k);
+        const long long on = plane(k == nz - 2 ? 1 : k + 1);
+        const bool kin = (k >= 1 && k <= nz - 2);
+        double2 pp[4], hn[4];
+        double eL[4], eR[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const double* F = cur.f[f];
+            pp[f] = ld2(F, on + cofs);
+            hn[f] = halo ? ld2(F, on + cofs + hoff) : zero;
+            eL[f] = needL ? F[oc + rowst + offL] : 0.0;
+            eR[f] = needR ? F[oc + rowst + offR] : 0.0;
         }
-        st2(out.f[q], idx, o);
+        const long long idx = oc + cofs;
+        const double2 r2 = ld2(rho, idx);
+        const double2 t2 = BUOY ? ld2(T, idx) : zero;
+        __syncthreads();
+        const int b = k & 1;
+        double kra[4] = {0.0, 0.0, 0.0, 0.0}, krb[4] = {0.0, 0.0, 0.0, 0.0};
+        const bool ina = kin && ina0, inb = kin && inb0;
+        if (ina || inb) {
+            const bool oka =
+                ina && !(r2.x <= 1e-10) && !(fabs(dxa0) < 1e-10) && !(fabs(dyj) < 1e-10);
+            const bool okb =
+                inb && !(r2.y <= 1e-10) && !(fabs(dxa1) < 1e-10) && !(fabs(dyj) < 1e-10);
+            auto diffs = [&](int f, RkD1& da, RkD1& db) __attribute__((always_inline)) {
+                const double2 c2 = rows[b][f][w + 1][lane];
+                double2 d2 = rows[b][f][w][lane], u2 = rows[b][f][w + 2][lane];
+                if (yw) {  // two rows of the grid: a direct load of the wrapped row
+                    const double2 yr = ld2(cur.f[f], oc + cofs + ywoff);
+                    if (j == 1) d2 = yr;
+                    if (j == ny - 2) u2 = yr;
+                }
+                const double2 m2 = rows[b ^ 1][f][w + 1][lane], p2 = pp[f];
+                const double l = __shfl_up(c2.y, 1, 64);
+                const double r = __shfl_down(c2.x, 1, 64);
+                const double xl = (lane == 0) ? eL[f] : l;
+                const double bl = (i0 == 0) ? eL[f] : c2.x;
+                const double ar = (i0 == nx - 2) ? eR[f] : c2.y;
+                const double xr = (lane == 63 || i0 + 1 == nx - 2) ? eR[f] : r;
+                rk_pair_diffs(rc, c2, d2, u2, m2, p2, xl, ar, bl, xr, dxa0, dxa1, dyj, da, db);
+            };
+            const double2 uc = rows[b][0][w + 1][lane], vc = rows[b][1][w + 1][lane],
+                          wc = rows[b][2][w + 1][lane];
+            rk_pair_kr<BUOY>(rc, diffs, uc, vc, wc, r2, t2, su, sv0, sv1, oka, okb, kra, krb);
+        }
+        if (valid) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rk_pair_update<STAGE>(rc, q0, acc, out, q, idx, kra[q], krb[q]);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            rows[b ^ 1][f][w + 1][lane] = pp[f];
+            if (halo) rows[b ^ 1][f][hslot][lane] = hn[f];
+        }
+        if (k == 0) {  // plane 1's z- neighbour is plane nz - 2 (own slots)
+            const long long om = plane(nz - 2);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) rows[b][f][w + 1][lane] = ld2(cur.f[f], om + cofs);
+        }
     }
 }
 
@@ -3193,12 +3382,17 @@ __device__ __forceinline__ void corr_reduce_n(double mv, double mp, bool bad,
     }
 }
 
+// FL & SW_PREFETCH (r03): the loads of plane k + 1's step (P centre and y
+// halo of plane k + 2, P's x-edge cells and u*, v*, w* of plane k + 1) are
+// issued before plane k is computed, so they land under its arithmetic and
+// barrier (k_cgB's bundle); otherwise a step's loads are issued at its top.
 template <int FL>
 static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
     SGeo g, CorrCoef2 cc, const double* __restrict__ us, const double* __restrict__ vs,
     const double* __restrict__ ws, const double* __restrict__ P, double* __restrict__ U,
     double* __restrict__ V, double* __restrict__ W, unsigned long long* red) {
     constexpr int TY = PC_TY;
+    constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     const RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
@@ -3209,19 +3403,48 @@ static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
     const bool xok = c.i0 < g.nx;
     const bool eok = (c.lane == 0 && c.i0 >= 1 && xok) || (c.lane == 63 && c.i0 + 2 < g.nx);
     const long long eoff = (c.lane == 0) ? -1 : 2;
-    const double2 zero = make_double2(0.0, 0.0);
     double mv = 0.0, mp = 0.0;
     bool bad = false;
     long long idx = c.idx;
+    // one step's loads: P of the next plane (centre, y halo), the x-edge P
+    // and u*, v*, w* of this plane
+    struct Bundle {
+        double2 pp, hn, qa, qb, qc;
+        double e;
+    };
+    auto issue = [&](long long ix) __attribute__((always_inline)) {
+        const double2 zero = make_double2(0.0, 0.0);
+        Bundle b;
+        b.pp = ld2(P, ix + g.sz);
+        b.hn = halo ? ld2(P, ix + g.sz + hoff) : zero;
+        b.e = eok ? P[ix + eoff] : 0.0;
+        b.qa = ld2v<FL>(us, ix);
+        b.qb = ld2v<FL>(vs, ix);
+        b.qc = ld2v<FL>(ws, ix);
+        return b;
+    };
     double2 pm = ld2(P, idx - g.sz), pcv = ld2(P, idx);
     rows[0][c.w + 1][c.lane] = pcv;  // publishing as in k_pred3
     if (halo) rows[0][hslot][c.lane] = ld2(P, idx + hoff);
+    Bundle cur;
+    if (PF) {
+        cur = issue(idx);
+        // the prologue's loads land before the march (see k_cgA): an empty
+        // asm that reads them makes the compiler issue and wait for them here
+        asm volatile("" ::"v"(cur.pp.x), "v"(cur.pp.y), "v"(cur.hn.x), "v"(cur.hn.y),
+                     "v"(cur.qa.x), "v"(cur.qa.y), "v"(cur.qb.x), "v"(cur.qb.y), "v"(cur.qc.x),
+                     "v"(cur.qc.y), "v"(cur.e));
+    }
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-        const double2 pp = ld2(P, idx + g.sz);
-        const double2 hn = halo ? ld2(P, idx + g.sz + hoff) : zero;
-        const double e = eok ? P[idx + eoff] : 0.0;
-        const double2 qa = ld2v<FL>(us, idx), qb = ld2v<FL>(vs, idx), qc = ld2v<FL>(ws, idx);
+        Bundle nxt;
+        if (PF) {
+            if (k + 1 < c.ke) nxt = issue(idx + g.ps);
+        } else {
+            cur = issue(idx);
+        }
+        const double2 pp = cur.pp, qa = cur.qa, qb = cur.qb, qc = cur.qc;
+        const double e = cur.e;
         __syncthreads();
         const double2 ys = rows[buf][c.w][c.lane];
         const double2 yn = rows[buf][c.w + 2][c.lane];
@@ -3275,7 +3498,8 @@ static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
         pcv = pp;
         buf ^= 1;
         rows[buf][c.w + 1][c.lane] = pp;
-        if (halo) rows[buf][hslot][c.lane] = hn;
+        if (halo) rows[buf][hslot][c.lane] = cur.hn;
+        if (PF) cur = nxt;
     }
     corr_reduce_n<TY>(mv, mp, bad, red);
 }

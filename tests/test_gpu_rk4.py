@@ -61,9 +61,17 @@ def _case(nx, ny, nz, buoy=False, energy=False):
     return g, f, p
 
 
+# 3-D shapes also cover k_rk_stage3's tiling (r03): nx = 130 / 131 put the
+# wrapped x neighbour (i0 = nx - 2 / i0 + 1 = nx - 2) on lane 0 of the second
+# 128-column tile, ny = 3 makes row 1 both wrapped rows, nz = 3 plane 1 both
+# wrapped planes, and 11 / 9 planes split the z-march into several runs
 @pytest.mark.parametrize("shape,buoy,energy", [((17, 13, 11), False, False),
                                                ((17, 13, 11), True, True),
-                                               ((20, 18, 1), True, False)])
+                                               ((20, 18, 1), True, False),
+                                               ((130, 19, 9), False, False),
+                                               ((131, 3, 7), True, False),
+                                               ((9, 17, 3), False, False),
+                                               ((257, 21, 5), True, True)])
 def test_rk4_steps_bitwise(hip_lib, shape, buoy, energy):
     g, f, p = _case(*shape, buoy=buoy, energy=energy)
     fo = api.FlowField(*shape)
