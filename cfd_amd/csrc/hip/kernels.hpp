@@ -625,29 +625,8 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     }
     Bundle cur;
     if (PF) cur = issue(c.kb, idx);
-    // (r03) the prologue's loads land before the march: otherwise the
-    // compiler's wait for a prologue register merges, at the loop's compute
-    // block, with the pending prefetch of the next plane into one vmcnt(0),
-    // i.e. every step waited for plane k + 1 before computing plane k (a
-    // builtin, not inline asm: the waitcnt pass sees only real waits; the
-    // empty asm keeps the prologue's loads above it)
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-        // p of plane k is known here: store it before the next plane's loads
-        // are issued (r03). Stored after them, the compiler's in-order vmcnt
-        // wait for the store (its source registers are reused by the step's
-        // arithmetic) also waited for the whole prefetch bundle, so plane
-        // k + 1's loads landed before plane k was computed. (FOLD reads the
-        // old p_{it-4} of plane k from pn in the bundle: its store stays after
-        // the step.)
-        if (!FOLD && c.act) {
-            double2 pw;
-            pw.x = c.in0 ? pc.x : 0.0;
-            pw.y = c.in1 ? pc.y : 0.0;
-            st2v<FL>(pn, idx, pw);
-        }
         Bundle nxt;
         if (PF) {
             if (k + 1 < c.ke) nxt = issue(k + 1, idx + g.ps);
@@ -676,7 +655,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
                          : cur.fxo.y;
             st2v<FL>(fx, idx, xw);
         }
-        if (FOLD && c.act) {
+        if (c.act) {
             double2 pw;
             pw.x = c.in0 ? pc.x : 0.0;
             pw.y = c.in1 ? pc.y : 0.0;
@@ -1672,7 +1651,7 @@ __global__ __launch_bounds__(256) void k_rk_stage(Geo g, RkCoef rc, Fld4 cur, Fl
 }
 
 // First and second differences of one field at the cells (i0, i0 + 1) of a
-// pair (r02b, shared by k_rk_stage2 / k_rk_stage3): c2 the pair, d2 / u2 the
+// pair (r02b): c2 the pair, d2 / u2 the
 // (periodically resolved) y- / y+ rows, m2 / p2 the z- / z+ planes, xl the
 // left of i0, ar the right of i0, bl the left of i0 + 1, xr the right of
 // i0 + 1. Same expressions and order as rk_rhs, so the values are bitwise.
@@ -1834,143 +1813,6 @@ __global__ __launch_bounds__(256) void k_rk_stage2(Geo g, RkCoef rc, Fld4 cur, F
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) rk_pair_update<STAGE>(rc, q0, acc, out, q, idx, kra[q], krb[q]);
-}
-
-// r03: the stage as a z-march over 128 x TY tiles with the y neighbours of
-// the four stencil fields from LDS (k_pred3's scheme): each wave owns one row,
-// the two edge waves also load the rows beyond the tile, every wave publishes
-// its centre row once per plane (rows double-buffered by plane parity, one
-// barrier per plane), and the z neighbours are a register ring, so u, v, w, p
-// are read from HBM once per stage instead of up to three times (k_rk_stage2
-// takes y / z neighbours from the caches). The march covers every plane of
-// the grid (the boundary planes take the pointwise update only). Periodic
-// neighbours (ns_momentum_rhs_scalar.h via solver_rk4.c): rows 1 / ny - 2 take
-// the wrapped row by a direct load, the ring takes plane nz - 2 as the z-
-// neighbour of plane 1 and plane nz - 2's z+ load is plane 1; x wraps and the
-// tile's x edges are one scalar load per side and field. Operands and order are
-// k_rk_stage2's (rk_pair_diffs / rk_pair_kr / rk_pair_update): bitwise. 3-D
-// grids (nz >= 3) on one device.
-template <int STAGE, bool BUOY, int TY>
-__global__ __launch_bounds__(64 * TY, 1) void k_rk_stage3(SGeo g, RkCoef rc, Fld4 cur, Fld4 q0,
-                                                         Fld4 acc, Fld4 out,
-                                                         const double* __restrict__ rho,
-                                                         const double* __restrict__ T,
-                                                         const double* __restrict__ dxa,
-                                                         const double* __restrict__ dya,
-                                                         const double* __restrict__ su_row,
-                                                         const double* __restrict__ sv_col) {
-    __shared__ double2 rows[2][4][TY + 2][64];
-    const RowPair c = row_pair<TY>(g);
-    const int lane = c.lane, w = c.w, i0 = c.i0, j = c.j;
-    const int nx = g.nx, ny = g.ny, nz = g.nz;
-    const bool halo = (w == 0) || (w == TY - 1);
-    const int jc = min(j, ny - 1);
-    const int jh = (w == 0) ? max(j - 1, 0) : min(j + 1, ny - 1);
-    const int hslot = (w == 0) ? 0 : TY + 1;
-    const long long hoff = (long long)(jh - jc) * g.px;
-    const bool valid = (i0 < nx) && (j < ny);   // the pair's cells are stored
-    const bool yin = (j >= 1 && j <= ny - 2);   // row j has interior cells
-    const bool ina0 = yin && i0 >= 1 && i0 <= nx - 2;
-    const bool inb0 = yin && i0 + 1 <= nx - 2;
-    // wrapped y rows: row 1 takes row ny - 2 as y-, row ny - 2 takes row 1 as
-    // y+ (one row holds both when ny == 3); wave-uniform
-    const bool yw = yin && (j == 1 || j == ny - 2);
-    const long long ywoff = (long long)((j == 1 ? ny - 2 : 1) - jc) * g.px;
-    // x neighbours outside the lane's pair: eL (lane 0: cell i0 - 1, or
-    // nx - 2 for i0 == 0), eR (cell 1 where the pair wraps: i0 == nx - 2 or
-    // i0 + 1 == nx - 2; else lane 63: cell i0 + 2)
-    const long long rowst = (long long)jc * g.px;  // row start in plane 0
-    const bool needL = valid && lane == 0 && (i0 == 0 || i0 >= 2);
-    const long long offL = (i0 == 0) ? (long long)(nx - 2) : (long long)(i0 - 1);
-    const bool wrapR = (i0 == nx - 2) || (i0 + 1 == nx - 2);
-    const bool needR = valid && (wrapR || (lane == 63 && i0 + 2 < nx));
-    const long long offR = wrapR ? 1LL : (long long)(i0 + 2);
-    const double dyj = dya[jc], su = su_row[jc];
-    const double dxa0 = i0 < nx ? dxa[i0] : 0.0, dxa1 = dxa[min(i0 + 1, nx - 1)];
-    const double sv0 = i0 < nx ? sv_col[i0] : 0.0, sv1 = sv_col[min(i0 + 1, nx - 1)];
-    const double2 zero = make_double2(0.0, 0.0);
-    auto plane = [&](int k) -> long long { return (long long)min(max(k, 0), nz - 1) * g.ps; };
-    const long long cofs = c.idx - c.kb * g.ps;  // the pair in plane 0
-    // LDS holds plane k's rows (centre and y halo) in rows[k & 1] and, in the
-    // centre slots of rows[(k & 1) ^ 1], plane k's z- neighbour (plane k - 1;
-    // plane nz - 2 for plane 1): a thread reads back only its own centre
-    // slot of the z- plane, which it alone rewrites (with plane k + 1) after
-    // the step, so only the y neighbours need the barrier. Registers carry
-    // just the loads of plane k + 1 (plane 1 at the step of plane nz - 2: the
-    // wrapped z+), so the march has no register ring.
-    {
-        const long long om = plane(c.kb == 1 ? nz - 2 : c.kb - 1);
-        const long long oc = plane(c.kb);
-        const int b0 = c.kb & 1;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            rows[b0 ^ 1][f][w + 1][lane] = ld2(cur.f[f], om + cofs);
-            rows[b0][f][w + 1][lane] = ld2(cur.f[f], oc + cofs);
-            if (halo) rows[b0][f][hslot][lane] = ld2(cur.f[f], oc + cofs + hoff);
-        }
-    }
-    for (int k = c.kb; k < c.ke; ++k) {
-        const long long oc = plane(k);
-        const long long on = plane(k == nz - 2 ? 1 : k + 1);
-        const bool kin = (k >= 1 && k <= nz - 2);
-        double2 pp[4], hn[4];
-        double eL[4], eR[4];
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            const double* F = cur.f[f];
-            pp[f] = ld2(F, on + cofs);
-            hn[f] = halo ? ld2(F, on + cofs + hoff) : zero;
-            eL[f] = needL ? F[oc + rowst + offL] : 0.0;
-            eR[f] = needR ? F[oc + rowst + offR] : 0.0;
-        }
-        const long long idx = oc + cofs;
-        const double2 r2 = ld2(rho, idx);
-        const double2 t2 = BUOY ? ld2(T, idx) : zero;
-        __syncthreads();
-        const int b = k & 1;
-        double kra[4] = {0.0, 0.0, 0.0, 0.0}, krb[4] = {0.0, 0.0, 0.0, 0.0};
-        const bool ina = kin && ina0, inb = kin && inb0;
-        if (ina || inb) {
-            const bool oka =
-                ina && !(r2.x <= 1e-10) && !(fabs(dxa0) < 1e-10) && !(fabs(dyj) < 1e-10);
-            const bool okb =
-                inb && !(r2.y <= 1e-10) && !(fabs(dxa1) < 1e-10) && !(fabs(dyj) < 1e-10);
-            auto diffs = [&](int f, RkD1& da, RkD1& db) __attribute__((always_inline)) {
-                const double2 c2 = rows[b][f][w + 1][lane];
-                double2 d2 = rows[b][f][w][lane], u2 = rows[b][f][w + 2][lane];
-                if (yw) {  // two rows of the grid: a direct load of the wrapped row
-                    const double2 yr = ld2(cur.f[f], oc + cofs + ywoff);
-                    if (j == 1) d2 = yr;
-                    if (j == ny - 2) u2 = yr;
-                }
-                const double2 m2 = rows[b ^ 1][f][w + 1][lane], p2 = pp[f];
-                const double l = __shfl_up(c2.y, 1, 64);
-                const double r = __shfl_down(c2.x, 1, 64);
-                const double xl = (lane == 0) ? eL[f] : l;
-                const double bl = (i0 == 0) ? eL[f] : c2.x;
-                const double ar = (i0 == nx - 2) ? eR[f] : c2.y;
-                const double xr = (lane == 63 || i0 + 1 == nx - 2) ? eR[f] : r;
-                rk_pair_diffs(rc, c2, d2, u2, m2, p2, xl, ar, bl, xr, dxa0, dxa1, dyj, da, db);
-            };
-            const double2 uc = rows[b][0][w + 1][lane], vc = rows[b][1][w + 1][lane],
-                          wc = rows[b][2][w + 1][lane];
-            rk_pair_kr<BUOY>(rc, diffs, uc, vc, wc, r2, t2, su, sv0, sv1, oka, okb, kra, krb);
-        }
-        if (valid) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rk_pair_update<STAGE>(rc, q0, acc, out, q, idx, kra[q], krb[q]);
-        }
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            rows[b ^ 1][f][w + 1][lane] = pp[f];
-            if (halo) rows[b ^ 1][f][hslot][lane] = hn[f];
-        }
-        if (k == 0) {  // plane 1's z- neighbour is plane nz - 2 (own slots)
-            const long long om = plane(nz - 2);
-#pragma unroll
-            for (int f = 0; f < 4; ++f) rows[b][f][w + 1][lane] = ld2(cur.f[f], om + cofs);
-        }
-    }
 }
 
 // max |u|, max |p| and the non-finite flag over the owned planes (the
@@ -3382,17 +3224,12 @@ __device__ __forceinline__ void corr_reduce_n(double mv, double mp, bool bad,
     }
 }
 
-// FL & SW_PREFETCH (r03): the loads of plane k + 1's step (P centre and y
-// halo of plane k + 2, P's x-edge cells and u*, v*, w* of plane k + 1) are
-// issued before plane k is computed, so they land under its arithmetic and
-// barrier (k_cgB's bundle); otherwise a step's loads are issued at its top.
 template <int FL>
 static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
     SGeo g, CorrCoef2 cc, const double* __restrict__ us, const double* __restrict__ vs,
     const double* __restrict__ ws, const double* __restrict__ P, double* __restrict__ U,
     double* __restrict__ V, double* __restrict__ W, unsigned long long* red) {
     constexpr int TY = PC_TY;
-    constexpr bool PF = (FL & SW_PREFETCH) != 0;
     __shared__ double2 rows[2][TY + 2][64];
     const RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
@@ -3403,48 +3240,19 @@ static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
     const bool xok = c.i0 < g.nx;
     const bool eok = (c.lane == 0 && c.i0 >= 1 && xok) || (c.lane == 63 && c.i0 + 2 < g.nx);
     const long long eoff = (c.lane == 0) ? -1 : 2;
+    const double2 zero = make_double2(0.0, 0.0);
     double mv = 0.0, mp = 0.0;
     bool bad = false;
     long long idx = c.idx;
-    // one step's loads: P of the next plane (centre, y halo), the x-edge P
-    // and u*, v*, w* of this plane
-    struct Bundle {
-        double2 pp, hn, qa, qb, qc;
-        double e;
-    };
-    auto issue = [&](long long ix) __attribute__((always_inline)) {
-        const double2 zero = make_double2(0.0, 0.0);
-        Bundle b;
-        b.pp = ld2(P, ix + g.sz);
-        b.hn = halo ? ld2(P, ix + g.sz + hoff) : zero;
-        b.e = eok ? P[ix + eoff] : 0.0;
-        b.qa = ld2v<FL>(us, ix);
-        b.qb = ld2v<FL>(vs, ix);
-        b.qc = ld2v<FL>(ws, ix);
-        return b;
-    };
     double2 pm = ld2(P, idx - g.sz), pcv = ld2(P, idx);
     rows[0][c.w + 1][c.lane] = pcv;  // publishing as in k_pred3
     if (halo) rows[0][hslot][c.lane] = ld2(P, idx + hoff);
-    Bundle cur;
-    if (PF) {
-        cur = issue(idx);
-        // the prologue's loads land before the march (see k_cgA): an empty
-        // asm that reads them makes the compiler issue and wait for them here
-        asm volatile("" ::"v"(cur.pp.x), "v"(cur.pp.y), "v"(cur.hn.x), "v"(cur.hn.y),
-                     "v"(cur.qa.x), "v"(cur.qa.y), "v"(cur.qb.x), "v"(cur.qb.y), "v"(cur.qc.x),
-                     "v"(cur.qc.y), "v"(cur.e));
-    }
     int buf = 0;
     for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
-        Bundle nxt;
-        if (PF) {
-            if (k + 1 < c.ke) nxt = issue(idx + g.ps);
-        } else {
-            cur = issue(idx);
-        }
-        const double2 pp = cur.pp, qa = cur.qa, qb = cur.qb, qc = cur.qc;
-        const double e = cur.e;
+        const double2 pp = ld2(P, idx + g.sz);
+        const double2 hn = halo ? ld2(P, idx + g.sz + hoff) : zero;
+        const double e = eok ? P[idx + eoff] : 0.0;
+        const double2 qa = ld2v<FL>(us, idx), qb = ld2v<FL>(vs, idx), qc = ld2v<FL>(ws, idx);
         __syncthreads();
         const double2 ys = rows[buf][c.w][c.lane];
         const double2 yn = rows[buf][c.w + 2][c.lane];
@@ -3498,8 +3306,7 @@ static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
         pcv = pp;
         buf ^= 1;
         rows[buf][c.w + 1][c.lane] = pp;
-        if (halo) rows[buf][hslot][c.lane] = cur.hn;
-        if (PF) cur = nxt;
+        if (halo) rows[buf][hslot][c.lane] = hn;
     }
     corr_reduce_n<TY>(mv, mp, bad, red);
 }

@@ -1051,7 +1051,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         c->pc3 = 1;
         if (const char* e = getenv("CFD_HIP_PC3")) {  // A/B: k_pred3 / k_corr3 (ctx.hpp)
             const int v = atoi(e);
-            c->pc3 = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+            c->pc3 = (v == 1 || v == 2 || v == 4) ? v : 0;
         }
     }
     c->split_b = (c->nranks > 1 && nint_k >= 3) ? 1 : 0;
@@ -1517,7 +1517,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                   c->pgeo16, pc, c->u, c->v, c->w, c->T, c->src_u_row,
                                   c->src_v_col, c->us, c->vs, c->ws);
         };
-        if (c->pc3 == 1 || c->pc3 == 8) {
+        if (c->pc3 == 1) {
             if (buoy) p3(k_pred3<true, 0>);
             else p3(k_pred3<false, 0>);
         } else if (c->pc3 == 2) {
@@ -1593,8 +1593,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                   c->pgeo16, cc, c->us, c->vs, c->ws, c->pn, c->u, c->v, c->w,
                                   c->red);
         };
-        if (c->pc3 == 8) c3(k_corr3<SW_PREFETCH>);
-        else if (c->pc3 == 1) c3(k_corr3<0>);
+        if (c->pc3 == 1) c3(k_corr3<0>);
         else if (c->pc3 == 2) c3(k_corr3<SW_NT_STORE>);
         else if (c->pc3 == 4) c3(k_corr3<SW_NT_STORE | SW_NT_LOAD>);
         else

@@ -33,55 +33,10 @@ static cfd_status_t ensure_rk(hip_proj_ctx* c) {
     return CFD_SUCCESS;
 }
 
-// k_rk_stage3 tiling: 128 x TY tiles marching z over every plane; runs of
-// up to 256 planes, halved until the grid has a workgroup per CU
-static SGeo rk3_geo(const hip_proj_ctx* c, int ty) {
-    SGeo q = c->sgeo;
-    const int nz = (int)c->geo.nz;
-    q.k0 = 0;
-    q.k1 = nz;
-    q.kmode = 0;
-    q.kofs = 0;
-    q.tiles_x = (int)((c->nx + 127) / 128);
-    q.tiles_y = (int)((c->ny + ty - 1) / ty);
-    q.kc = 256;
-    while (q.kc > 4 &&
-           (long long)q.tiles_x * q.tiles_y * ((nz + q.kc - 1) / q.kc) < c->grid_cap / 8)
-        q.kc /= 2;
-    q.kc = std::max(1, std::min(q.kc, nz));
-    q.tiles_z = (nz + q.kc - 1) / q.kc;
-    return q;
-}
-
 template <int S>
 static void launch_stage(hip_proj_ctx* c, bool buoy, const RkCoef& rc, const Fld4& cur,
                          const Fld4& q0, const Fld4& acc, const Fld4& out) {
-    // z-marched stage with LDS y rows (default on 3-D grids, 8-row tiles:
-    // 209 VGPRs, no spills; 16 rows spill ~100); CFD_HIP_RK3 = 0 selects the
-    // x-pair kernel, 16 the 16-row tiles
-    static const int rk3 = [] {
-        const char* e = getenv("CFD_HIP_RK3");
-        const int v = e ? atoi(e) : 8;
-        return (v == 8 || v == 16) ? v : 0;
-    }();
-    if (rk3 && c->geo.nz >= 3 && c->geo.sz) {
-        const SGeo q = rk3_geo(c, rk3);
-        const dim3 nb((unsigned)(q.tiles_x * q.tiles_y * q.tiles_z));
-        auto go = [&](auto kern, int ty) {
-            hipExtLaunchKernelGGL(kern, nb, dim3(64 * ty), 0, c->stream, c->ta, c->tb, 0, q, rc,
-                                  cur, q0, acc, out, c->rho, c->T, c->dxa, c->dya, c->src_u_row,
-                                  c->src_v_col);
-        };
-        if (rk3 == 16) {
-            if (buoy) go(k_rk_stage3<S, true, 16>, 16);
-            else go(k_rk_stage3<S, false, 16>, 16);
-        } else {
-            if (buoy) go(k_rk_stage3<S, true, 8>, 8);
-            else go(k_rk_stage3<S, false, 8>, 8);
-        }
-        return;
-    }
-    // x-pair stage kernel; CFD_HIP_RK_PAIR=0 selects the per-cell one
+    // x-pair stage kernel (default); CFD_HIP_RK_PAIR=0 selects the per-cell one
     static const bool pair = !(getenv("CFD_HIP_RK_PAIR") && atoi(getenv("CFD_HIP_RK_PAIR")) == 0);
     if (pair) {
         const dim3 g2((unsigned)((c->nx + 127) / 128), (unsigned)((c->ny + 3) / 4),
