@@ -421,6 +421,9 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     const unsigned nb = (unsigned)sweep_grid(c);
     const unsigned TH = 64u * (unsigned)c->sweep_ty;
     constexpr int FL = SW_NT_STORE | SW_NT_LOAD | SW_PREFETCH | SW_EDGE1;
+    // k_rb1: plain rhs loads (its tiles' rhs halo rows are re-read by the
+    // neighbouring tile; see the one-device launch below)
+    constexpr int FLR = SW_NT_STORE | SW_PREFETCH | SW_EDGE1;
     auto sweep = [&](int mode, const double* xi, double* xo, int it) {
         timed(c, HIP_KT_RELAX, [&] {
 #define RX_LAUNCH(TYV, M, DV)                                                                  \
@@ -486,7 +489,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             auto rb1 = [&](const SGeo& sg) {
                 const unsigned nbx = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
                 timed(c, HIP_KT_RELAX, [&] {
-                    hipExtLaunchKernelGGL((k_rb1<FL, 64, true, true>), dim3(nbx), dim3(1024), 0,
+                    hipExtLaunchKernelGGL((k_rb1<FLR, 64, true, true>), dim3(nbx), dim3(1024), 0,
                                           c->stream, c->ta, c->tb, 0, sg, rc, xi, xo, c->rhs,
                                           c->rxst, c->partials, c->counter, it, (const double*)RH,
                                           c->geo.lo_face ? 0 : 1, c->geo.hi_face ? 0 : 1, mb,
@@ -538,8 +541,19 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             // end-of-step loads (experiments)
             static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
                                          atoi(getenv("CFD_HIP_RB1_PF")) == 0);
+            // memory hints of k_rb1 / k_rb1m (SW_* bits): FLR = 13, NT stores
+            // of Y and plain rhs loads (r03: the NT rhs loads of 15 made the
+            // neighbouring tiles re-fetch the rhs halo rows; 512^3 0.744 ->
+            // 0.726 ms, 1024^2 x 512 2.925 -> 2.85 ms, fetch 19.6 -> 18.7
+            // B/cell, profiles/r03_rbfl.jsonl); CFD_HIP_RB1_FL = 12 / 14 / 15
+            // select the other hint sets (A/B)
+            static const int rb1_fl = [] {
+                const char* e = getenv("CFD_HIP_RB1_FL");
+                const int v = e ? atoi(e) : FLR;
+                return (v == 12 || v == 14 || v == 15) ? v : FLR;
+            }();
 #define RB1_LAUNCH(TCV, PFV)                                                                   \
-    hipExtLaunchKernelGGL((k_rb1<FL, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
+    hipExtLaunchKernelGGL((k_rb1<FLR, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
                           c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
                           c->counter, it, (const double*)nullptr, 0, 0, (Mbox*)nullptr,        \
                           (unsigned long long*)nullptr, neu_fold ? 1 : 0)
@@ -550,13 +564,30 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                 const int nbm = gm.tiles_x * gm.tiles_y * gm.tiles_z;
                 const unsigned nbt = (unsigned)(nbm + gs.tiles_x * gs.tiles_y * gs.tiles_z);
                 timed(c, HIP_KT_RELAX, [&] {
-                    hipExtLaunchKernelGGL((k_rb1m<FL, 16>), dim3(nbt), dim3(1024), 0, c->stream,
-                                          c->ta, c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs,
-                                          c->rxst, c->partials, c->counter, it, neu_fold ? 1 : 0);
+                    auto go = [&](auto kern) {
+                        hipExtLaunchKernelGGL(kern, dim3(nbt), dim3(1024), 0, c->stream, c->ta,
+                                              c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs, c->rxst,
+                                              c->partials, c->counter, it, neu_fold ? 1 : 0);
+                    };
+                    if (rb1_fl == 12) go(k_rb1m<12, 16>);
+                    else if (rb1_fl == 14) go(k_rb1m<14, 16>);
+                    else if (rb1_fl == 15) go(k_rb1m<15, 16>);
+                    else go(k_rb1m<FLR, 16>);
                 }, it);
             } else
             timed(c, HIP_KT_RELAX, [&] {
-                if (!rb1_pf) RB1_LAUNCH(64, false);
+                auto go = [&](auto kern) {
+                    hipExtLaunchKernelGGL(kern, dim3(nb1), dim3(1024), 0, c->stream, c->ta, c->tb,
+                                          0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,
+                                          c->counter, it, (const double*)nullptr, 0, 0,
+                                          (Mbox*)nullptr, (unsigned long long*)nullptr,
+                                          neu_fold ? 1 : 0);
+                };
+                if (rb1_pf && c->rb1_tc == 64 && rb1_fl != FLR) {
+                    if (rb1_fl == 12) go(k_rb1<12, 64, true>);
+                    else if (rb1_fl == 14) go(k_rb1<14, 64, true>);
+                    else go(k_rb1<15, 64, true>);
+                } else if (!rb1_pf) RB1_LAUNCH(64, false);
                 else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
                 else if (c->rb1_tc == 16) RB1_LAUNCH(16, true);
                 else RB1_LAUNCH(64, true);
