@@ -2328,7 +2328,7 @@ struct Rb1Lds {
 
 // The body of k_rb1 for the tile width TC; bid = this workgroup's tile-block
 // index within its geometry g (k_rb1m runs two geometries in one grid).
-template <int FL, int TC, bool PF, bool DIST, int PD = 0>
+template <int FL, int TC, bool PF, bool DIST>
 __device__ __forceinline__ void rb1_body(
     Rb1Lds& L, int bid, SGeo g, RelaxCoef rc, const double* __restrict__ X,
     double* __restrict__ Y, const double* __restrict__ rhs, RxState* st, double* partials,
@@ -2435,20 +2435,14 @@ __device__ __forceinline__ void rb1_body(
     // a full step of latency hiding, and no register copy of a loaded value
     // (a copy would wait for the load). Without PF the loads are issued at
     // the end of step q and the three X planes shift through xm, xc, xp.
-    // PD = 1 (r03 A/B): one more plane in flight, X in a six-slot ring and
-    // rhs in a three-slot ring (z loop unrolled by six); step q then issues
-    // X_{q+4} and rhs_{q+3}
-    constexpr int NXR = PD ? 6 : 4, NRR = PD ? 3 : 2;
-    double2 xr[NXR], br[NRR], rm;
+    double2 xr[4], br[2], rm;
     double bmh, rmmh;
     xr[0] = ldx(kb - 2);
     xr[1] = ldx(kb - 1);
     xr[2] = ldx(kb);
-    xr[3] = PD ? ldx(kb + 1) : zero;
-    if constexpr (PD) xr[4] = xr[5] = zero;
+    xr[3] = zero;
     br[0] = ldr(kb - 1);
-    br[1] = PD ? ldr(kb) : zero;
-    if constexpr (PD) br[2] = zero;
+    br[1] = zero;
     rm = zero;
     bmh = rmmh = 0.0;
     lput(xb, (kb - 1) & 1, r, c, xr[1]);
@@ -2458,12 +2452,11 @@ __device__ __forceinline__ void rb1_body(
     auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
         constexpr bool E = decltype(Ec)::value;
         constexpr int P = PF ? decltype(Pc)::value : 0;  // ring phase
-        constexpr int IM = P % NXR, IC = (P + 1) % NXR, IP = (P + 2) % NXR,
-                      IN = (P + 3 + PD) % NXR;
-        constexpr int BQ = P % NRR, BN = (P + 1 + PD) % NRR;
+        constexpr int IM = P & 3, IC = (P + 1) & 3, IP = (P + 2) & 3, IN = (P + 3) & 3;
+        constexpr int BQ = P & 1, BN = (P + 1) & 1;
         if constexpr (PF) {
-            xr[IN] = ldx(q + 3 + PD);
-            br[BN] = ldr(q + 2 + PD);
+            xr[IN] = ldx(q + 3);
+            br[BN] = ldr(q + 2);
         }
         const double2 xm = xr[IM], xc = xr[IC], xp = xr[IP], bq = br[BQ];
         __syncthreads();
@@ -2566,21 +2559,7 @@ __device__ __forceinline__ void rb1_body(
         constexpr bool A = decltype(E0c)::value;
         using TA = BoolC<A>;
         using TB = BoolC<!A>;
-        if constexpr (PF && PD) {
-            for (; q + 5 < ke; q += 6) {
-                step(TA{}, IntC<0>{}, q);
-                step(TB{}, IntC<1>{}, q + 1);
-                step(TA{}, IntC<2>{}, q + 2);
-                step(TB{}, IntC<3>{}, q + 3);
-                step(TA{}, IntC<4>{}, q + 4);
-                step(TB{}, IntC<5>{}, q + 5);
-            }
-            if (q < ke) step(TA{}, IntC<0>{}, q);
-            if (q + 1 < ke) step(TB{}, IntC<1>{}, q + 1);
-            if (q + 2 < ke) step(TA{}, IntC<2>{}, q + 2);
-            if (q + 3 < ke) step(TB{}, IntC<3>{}, q + 3);
-            if (q + 4 < ke) step(TA{}, IntC<4>{}, q + 4);
-        } else if constexpr (PF) {
+        if constexpr (PF) {
             for (; q + 3 < ke; q += 4) {
                 step(TA{}, IntC<0>{}, q);
                 step(TB{}, IntC<1>{}, q + 1);
@@ -2645,14 +2624,14 @@ __device__ __forceinline__ void rb1_body(
     }
 }
 
-template <int FL, int TC, bool PF, bool DIST = false, int PD = 0>
+template <int FL, int TC, bool PF, bool DIST = false>
 static __global__ __launch_bounds__(1024, 4) void k_rb1(
     SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
     const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
     const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred,
     int neu) {
     __shared__ Rb1Lds L;
-    rb1_body<FL, TC, PF, DIST, PD>(L, blockIdx.x, g, rc, X, Y, rhs, st, partials, counter, it, RH,
+    rb1_body<FL, TC, PF, DIST>(L, blockIdx.x, g, rc, X, Y, rhs, st, partials, counter, it, RH,
                                rh_lo, rh_hi, mb, dred, neu);
 }
 
@@ -2663,19 +2642,18 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
 // of 124); the strip's TC-16 / TC-32 tiles are 60 / 28 rows tall, so the
 // column strip needs 4.8x / 2.2x fewer workgroups. Both geometries share the
 // grid-wide residual reduction (part_total 0: gridDim.x workgroups).
-template <int FL, int TC2, int PD = 0>
+template <int FL, int TC2>
 static __global__ __launch_bounds__(1024, 4) void k_rb1m(
     SGeo g64, SGeo g2, int nb64, RelaxCoef rc, const double* __restrict__ X,
     double* __restrict__ Y, const double* __restrict__ rhs, RxState* st, double* partials,
     unsigned* counter, int it, int neu) {
     __shared__ Rb1Lds L;
     if ((int)blockIdx.x < nb64)
-        rb1_body<FL, 64, true, false, PD>(L, blockIdx.x, g64, rc, X, Y, rhs, st, partials,
-                                          counter, it, nullptr, 0, 0, nullptr, nullptr, neu);
+        rb1_body<FL, 64, true, false>(L, blockIdx.x, g64, rc, X, Y, rhs, st, partials, counter,
+                                      it, nullptr, 0, 0, nullptr, nullptr, neu);
     else
-        rb1_body<FL, TC2, true, false, PD>(L, blockIdx.x - nb64, g2, rc, X, Y, rhs, st,
-                                           partials, counter, it, nullptr, 0, 0, nullptr, nullptr,
-                                           neu);
+        rb1_body<FL, TC2, true, false>(L, blockIdx.x - nb64, g2, rc, X, Y, rhs, st, partials,
+                                       counter, it, nullptr, 0, 0, nullptr, nullptr, neu);
 }
 
 // R (the first colour SOR-updated, linear_solver_redblack.c:97-114) of a

@@ -547,8 +547,6 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             // 0.726 ms, 1024^2 x 512 2.925 -> 2.85 ms, fetch 19.6 -> 18.7
             // B/cell, profiles/r03_rbfl.jsonl); CFD_HIP_RB1_FL = 12 / 14 / 15
             // select the other hint sets (A/B)
-            // CFD_HIP_RB1_PD = 1: one more plane of loads in flight (A/B)
-            static const bool rb1_pd = getenv("CFD_HIP_RB1_PD") && atoi(getenv("CFD_HIP_RB1_PD")) == 1;
             static const int rb1_fl = [] {
                 const char* e = getenv("CFD_HIP_RB1_FL");
                 const int v = e ? atoi(e) : FLR;
@@ -571,8 +569,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                                               c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs, c->rxst,
                                               c->partials, c->counter, it, neu_fold ? 1 : 0);
                     };
-                    if (rb1_pd) go(k_rb1m<FLR, 16, 1>);
-                    else if (rb1_fl == 12) go(k_rb1m<12, 16>);
+                    if (rb1_fl == 12) go(k_rb1m<12, 16>);
                     else if (rb1_fl == 14) go(k_rb1m<14, 16>);
                     else if (rb1_fl == 15) go(k_rb1m<15, 16>);
                     else go(k_rb1m<FLR, 16>);
@@ -586,9 +583,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                                           (Mbox*)nullptr, (unsigned long long*)nullptr,
                                           neu_fold ? 1 : 0);
                 };
-                if (rb1_pd && rb1_pf && c->rb1_tc == 64) {
-                    go(k_rb1<FLR, 64, true, false, 1>);
-                } else if (rb1_pf && c->rb1_tc == 64 && rb1_fl != FLR) {
+                if (rb1_pf && c->rb1_tc == 64 && rb1_fl != FLR) {
                     if (rb1_fl == 12) go(k_rb1<12, 64, true>);
                     else if (rb1_fl == 14) go(k_rb1<14, 64, true>);
                     else go(k_rb1<15, 64, true>);
