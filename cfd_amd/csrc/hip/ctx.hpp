@@ -74,7 +74,6 @@ struct hip_proj_ctx {
     int rb1_tc = 64;           // k_rb1 tile width in x pairs (64, 32, 16)
     SGeo pgeo{};               // predictor / corrector z-march tiling (k_pred2, k_corr2)
     SGeo pgeo16{};             // k_pred3 / k_corr3: 128 x 16 tiles, y rows in LDS
-    SGeo pgeo8{};              // the same with 128 x 8 tiles (A/B, pc3 = 16)
     int pc3 = 1;  // 0: k_pred2 / k_corr2; k_pred3 / k_corr3 with 1: FL 0 (default), 2: NT stores, 4: + NT loads
     int split_b = 0;
     int sweep_ty = 8;  // waves (y rows) per CG sweep workgroup

@@ -3098,16 +3098,14 @@ static __global__ __launch_bounds__(64 * PR_TY, PF ? 3 : 4) void k_corr2(
 // non-temporal loads of the pointwise inputs (the corrector's u*, v*, w*).
 // ---------------------------------------------------------------------------
 constexpr int PC_TY = 16;
-// TY = 8 (r03 A/B): 512-thread workgroups, two per CU (<= 128 VGPRs)
-template <int TY>
-constexpr int pc_min_waves() { return TY == 16 ? 1 : 4; }
 
-template <bool BUOY, int FL, int TY = PC_TY>
-static __global__ __launch_bounds__(64 * TY, pc_min_waves<TY>()) void k_pred3(
+template <bool BUOY, int FL>
+static __global__ __launch_bounds__(64 * PC_TY, 1) void k_pred3(
     SGeo g, PredCoef2 pc, const double* __restrict__ U, const double* __restrict__ V,
     const double* __restrict__ W, const double* __restrict__ T,
     const double* __restrict__ src_u_row, const double* __restrict__ src_v_col,
     double* __restrict__ us, double* __restrict__ vs, double* __restrict__ ws) {
+    constexpr int TY = PC_TY;
     __shared__ double2 rows[2][3][TY + 2][64];
     const RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);
@@ -3226,11 +3224,12 @@ __device__ __forceinline__ void corr_reduce_n(double mv, double mp, bool bad,
     }
 }
 
-template <int FL, int TY = PC_TY>
-static __global__ __launch_bounds__(64 * TY, pc_min_waves<TY>()) void k_corr3(
+template <int FL>
+static __global__ __launch_bounds__(64 * PC_TY, 1) void k_corr3(
     SGeo g, CorrCoef2 cc, const double* __restrict__ us, const double* __restrict__ vs,
     const double* __restrict__ ws, const double* __restrict__ P, double* __restrict__ U,
     double* __restrict__ V, double* __restrict__ W, unsigned long long* red) {
+    constexpr int TY = PC_TY;
     __shared__ double2 rows[2][TY + 2][64];
     const RowPair c = row_pair<TY>(g);
     const bool halo = (c.w == 0) || (c.w == TY - 1);

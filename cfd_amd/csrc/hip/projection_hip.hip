@@ -1076,24 +1076,13 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             p3.kc /= 2;
         p3.kc = std::max(1, std::min(p3.kc, nint_k));
         p3.tiles_z = (nint_k + p3.kc - 1) / p3.kc;
-        // CFD_HIP_PC3=16 (A/B): 128 x 8 tiles, two 512-thread workgroups per
-        // CU, runs shortened until there are two per CU
-        SGeo& p8 = c->pgeo8;
-        p8 = p3;
-        p8.tiles_y = (int)((ny + 7) / 8);
-        p8.kc = 256;
-        while (p8.kc > 4 && (long long)p8.tiles_x * p8.tiles_y * ((nint_k + p8.kc - 1) / p8.kc) <
-                                c->grid_cap / 4)
-            p8.kc /= 2;
-        p8.kc = std::max(1, std::min(p8.kc, nint_k));
-        p8.tiles_z = (nint_k + p8.kc - 1) / p8.kc;
         // default k_pred3 / k_corr3 (r03: predictor 1.47 -> 1.25 ms, fetch
         // 45.7 -> 25.6 B/cell at 512^3, profiles/r03_pc3.jsonl);
         // CFD_HIP_PC3=0 selects k_pred2 / k_corr2
         c->pc3 = 1;
         if (const char* e = getenv("CFD_HIP_PC3")) {  // A/B: k_pred3 / k_corr3 (ctx.hpp)
             const int v = atoi(e);
-            c->pc3 = (v == 1 || v == 2 || v == 4 || v == 16) ? v : 0;
+            c->pc3 = (v == 1 || v == 2 || v == 4) ? v : 0;
         }
     }
     c->split_b = (c->nranks > 1 && nint_k >= 3) ? 1 : 0;
@@ -1559,17 +1548,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                   c->pgeo16, pc, c->u, c->v, c->w, c->T, c->src_u_row,
                                   c->src_v_col, c->us, c->vs, c->ws);
         };
-        if (c->pc3 == 16) {
-            const unsigned n8 =
-                (unsigned)(c->pgeo8.tiles_x * c->pgeo8.tiles_y * c->pgeo8.tiles_z);
-            auto p8 = [&](auto kern) {
-                hipExtLaunchKernelGGL(kern, dim3(n8), dim3(64 * 8), 0, c->stream, c->ta, c->tb,
-                                      0, c->pgeo8, pc, c->u, c->v, c->w, c->T, c->src_u_row,
-                                      c->src_v_col, c->us, c->vs, c->ws);
-            };
-            if (buoy) p8(k_pred3<true, 0, 8>);
-            else p8(k_pred3<false, 0, 8>);
-        } else if (c->pc3 == 1) {
+        if (c->pc3 == 1) {
             if (buoy) p3(k_pred3<true, 0>);
             else p3(k_pred3<false, 0>);
         } else if (c->pc3 == 2) {
@@ -1645,13 +1624,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
                                   c->pgeo16, cc, c->us, c->vs, c->ws, c->pn, c->u, c->v, c->w,
                                   c->red);
         };
-        if (c->pc3 == 16) {
-            const unsigned n8 =
-                (unsigned)(c->pgeo8.tiles_x * c->pgeo8.tiles_y * c->pgeo8.tiles_z);
-            hipExtLaunchKernelGGL((k_corr3<0, 8>), dim3(n8), dim3(64 * 8), 0, c->stream, c->ta,
-                                  c->tb, 0, c->pgeo8, cc, c->us, c->vs, c->ws, c->pn, c->u,
-                                  c->v, c->w, c->red);
-        } else if (c->pc3 == 1) c3(k_corr3<0>);
+        if (c->pc3 == 1) c3(k_corr3<0>);
         else if (c->pc3 == 2) c3(k_corr3<SW_NT_STORE>);
         else if (c->pc3 == 4) c3(k_corr3<SW_NT_STORE | SW_NT_LOAD>);
         else
