@@ -150,6 +150,8 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_config_default", A.HipProjConfig)
     _sig(lib, "cfd_hip_stream_bench", C.c_int, C.c_int, C.c_size_t, C.c_int,
          P(C.c_double), P(C.c_double))
+    _sig(lib, "cfd_hip_stream_bench_nm", C.c_int, C.c_int, C.c_size_t, C.c_int, C.c_int, C.c_int,
+         P(C.c_double))
     _sig(lib, "hip_projection_available", C.c_int)
     _sig(lib, "hip_proj_create", V, C.c_size_t, C.c_size_t, C.c_size_t, P(A.HipProjConfig))
     _sig(lib, "hip_proj_destroy", None, V)

@@ -93,7 +93,112 @@ void triad_u(int u, hipStream_t s, double2* a, const double2* b, const double2* 
     }
 }
 
+// NI streamed inputs, NO streamed outputs (r03): out_o = sum of the inputs
+// scaled by (o + 1); the roof of a kernel with that stream mix (the
+// predictor: 3 / 3, the corrector: 4 / 3, the CG sweeps: 2 / 1).
+constexpr int NM_MAX = 8;
+struct Ptrs {
+    double2* p[NM_MAX];
+};
+
+template <int NI, int NO, int U>
+__global__ __launch_bounds__(256) void k_stream_nm(Ptrs in, Ptrs out, size_t n2) {
+    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    double2 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * 256;
+            const double2 v = i < n2 ? in.p[q][i] : make_double2(0.0, 0.0);
+            acc[u].x += v.x;
+            acc[u].y += v.y;
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * 256;
+            if (i < n2) out.p[o][i] = make_double2(acc[u].x * (o + 1), acc[u].y * (o + 1));
+        }
+    }
+}
+
+template <int NI, int NO>
+void launch_nm(int u, hipStream_t s, const Ptrs& in, const Ptrs& out, size_t n2) {
+    auto go = [&](auto kern, int uu) {
+        const unsigned g = (unsigned)((n2 + 256 * uu - 1) / (256 * uu));
+        hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, s, in, out, n2);
+    };
+    if (u == 1) go(k_stream_nm<NI, NO, 1>, 1);
+    else if (u == 2) go(k_stream_nm<NI, NO, 2>, 2);
+    else go(k_stream_nm<NI, NO, 4>, 4);
+}
+
+bool nm_u(int ni, int no, int u, hipStream_t s, const Ptrs& in, const Ptrs& out, size_t n2) {
+#define NM_CASE(I, O) \
+    if (ni == I && no == O) return launch_nm<I, O>(u, s, in, out, n2), true;
+    NM_CASE(1, 1) NM_CASE(2, 1) NM_CASE(3, 1) NM_CASE(2, 2) NM_CASE(3, 3) NM_CASE(4, 3)
+    NM_CASE(4, 4) NM_CASE(5, 3)
+#undef NM_CASE
+    return false;
+}
+
 }  // namespace
+
+// Streamed fp64 arrays of n elements each, `ni` read and `no` written per
+// element (built pairs: 1/1, 2/1, 3/1, 2/2, 3/3, 4/3, 4/4, 5/3); best of
+// `reps` timed rounds over 1-4 loads per lane, bytes (ni + no) x 8 per element.
+extern "C" cfd_status_t cfd_hip_stream_bench_nm(int device, size_t n, int ni, int no, int reps,
+                                                double* gbps) {
+    if (!gbps || n < 2 || reps < 1 || ni < 1 || no < 1 || ni > 5 || no > 4) return CFD_ERROR_INVALID;
+    *gbps = 0.0;
+    if (hipSetDevice(device) != hipSuccess) return CFD_ERROR_UNSUPPORTED;
+    const size_t n2 = n / 2;
+    Ptrs in{}, out{};
+    double2* bufs[NM_MAX] = {};
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    cfd_status_t st = CFD_ERROR;
+    bool ok = hipStreamCreate(&s) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
+              hipEventCreate(&e1) == hipSuccess;
+    for (int q = 0; q < ni + no && ok; ++q) {
+        ok = hipMalloc(&bufs[q], n2 * sizeof(double2)) == hipSuccess;
+        if (ok) hipLaunchKernelGGL(k_stream_init, dim3(2048), dim3(256), 0, s, bufs[q], bufs[q],
+                                   bufs[q], n2);
+    }
+    if (ok) {
+        for (int q = 0; q < ni; ++q) in.p[q] = bufs[q];
+        for (int o = 0; o < no; ++o) out.p[o] = bufs[ni + o];
+        double best = 1e30;
+        for (int u = 1; u <= 4 && ok; u *= 2) {
+            for (int r = 0; r < reps + 1 && ok; ++r) {
+                float ms = 0.f;
+                hipEventRecord(e0, s);
+                ok = nm_u(ni, no, u, s, in, out, n2);
+                hipEventRecord(e1, s);
+                ok = ok && hipEventSynchronize(e1) == hipSuccess &&
+                     hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+                if (ok && r > 0) best = std::min(best, (double)ms);
+            }
+        }
+        if (ok) {
+            *gbps = (double)(ni + no) * (double)(2 * n2) * sizeof(double) / (best * 1e-3) / 1e9;
+            st = CFD_SUCCESS;
+        } else {
+            st = CFD_ERROR_INVALID;
+        }
+    }
+    for (double2* b : bufs)
+        if (b) hipFree(b);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    if (s) hipStreamDestroy(s);
+    return st;
+}
 
 extern "C" cfd_status_t cfd_hip_stream_bench(int device, size_t n, int reps, double* copy_gbps,
                                              double* triad_gbps) {

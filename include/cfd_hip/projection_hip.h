@@ -264,6 +264,13 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_field_crc32(hip_proj_ctx_t* ctx, int field_
  * bench.py reports beside the 8 TB/s spec. */
 CFD_HIP_EXPORT cfd_status_t cfd_hip_stream_bench(int device, size_t n, int reps,
                                                  double* copy_gbps, double* triad_gbps);
+/* Measurement helper (not a reference interface): `ni` streamed fp64 inputs
+ * and `no` streamed outputs of n elements (pairs built: 1/1, 2/1, 3/1, 2/2,
+ * 3/3, 4/3, 4/4, 5/3; others CFD_ERROR_INVALID), best of `reps` rounds, in GB/s
+ * of (ni + no) x 8 B per element: the achievable rate of a kernel with that
+ * stream mix (the predictor 3/3, the corrector 4/3, the CG sweeps 2/1). */
+CFD_HIP_EXPORT cfd_status_t cfd_hip_stream_bench_nm(int device, size_t n, int ni, int no,
+                                                    int reps, double* gbps);
 
 /* VTK output of the resident state (vtk_output.c:196-275, write_vtk_flow_field
  * text): velocity, pressure, density (the resident per-cell rho, else rho0),
