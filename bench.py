@@ -546,11 +546,13 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
     """(timer, kernel symbol as rocprofv3 prints it, algorithmic B/cell) of the
     CG sweeps a run launches; the symbols key the committed PMC profile."""
     d = "true" if dist_ else "false"
+    # sweep B marches z downwards on one device (CFD_HIP_CGB_REV=0: upwards)
+    rev = "true" if (not dist_ and os.environ.get("CFD_HIP_CGB_REV", "1") != "0") else "false"
     if cg_variant == 1:
         return (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
                 ("cc_spmv", f"k_cc2<{rows}, {d}, false>", BYTES_CC_SPMV))
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
-            ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}>", BYTES_SWEEP_B),
+            ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, {rev}>", BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))
 
 

@@ -708,7 +708,13 @@ struct PPrev {
     const double* q[CG_XFOLD - 1];  // p_{it-3}, p_{it-2}, p_{it-1}
 };
 
-template <int TY, bool DIST, int FL = 0>
+// REV (r03, one device, 3-D): the tile marches z downwards. Sweep A marches
+// upwards, so each sweep starts on the planes the previous one touched last,
+// which the 256 MB Infinity Cache still holds (p just written by sweep A,
+// r just read by it; then r just written by sweep B for the next sweep A).
+// The z neighbours keep their roles in lap7, so A p is bitwise sweep A's; only
+// the order of the (r, r) partial sums within a tile changes.
+template <int TY, bool DIST, int FL = 0, bool REV = false>
 static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     SGeo g, Lap L, const double* __restrict__ p, double* __restrict__ r, CgState* st,
     double* partials, unsigned* counter, int it, double* dsum, Mbox* mb) {
@@ -737,13 +743,17 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         double2 pp, hp, rr;
         double el, er;
     };
+    // sd: the z stride towards the next plane of the march
+    const long long sd = REV ? -g.sz : g.sz;
+    const long long pstep = REV ? -g.ps : g.ps;
     auto issue = [&](int k, long long ix) __attribute__((always_inline)) {
         const double2 zero = make_double2(0.0, 0.0);  // a value, not the captured object
         Bundle b;
-        const long long ip = ix + g.sz;
+        const long long ip = ix + sd;
+        const bool more = REV ? (k - 1 >= c.kb) : (k + 1 < c.ke);
         if (inner) b.pp = xok ? ld2n<true>(p, ip) : zero;
         else b.pp = xok ? ld2(p, ip) : zero;
-        b.hp = (xok && halo && k + 1 < c.ke) ? ld2(p, ip + hoff) : zero;
+        b.hp = (xok && halo && more) ? ld2(p, ip + hoff) : zero;
         b.rr = xok ? ld2v<FL>(r, ix) : zero;
         if (E1) {
             b.el = eok ? p[ix + eoff] : 0.0;
@@ -755,17 +765,19 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         return b;
     };
     double acc = 0.0;
-    long long idx = c.idx;
-    double2 pm = xok ? ld2(p, idx - g.sz) : zero;
+    const int k_first = REV ? c.ke - 1 : c.kb;
+    long long idx = c.idx + (REV ? (long long)(c.ke - 1 - c.kb) * g.ps : 0LL);
+    // pm: the plane the march left (z- forwards, z+ in REV), pp: the next one
+    double2 pm = xok ? ld2(p, idx - sd) : zero;
     double2 pc = xok ? ld2(p, idx) : zero;
     double2 hc = (xok && halo) ? ld2(p, idx + hoff) : zero;
     Bundle cur;
-    if (PF) cur = issue(c.kb, idx);
+    if (PF) cur = issue(k_first, idx);
     int buf = 0;
-    for (int k = c.kb; k < c.ke; ++k, idx += g.ps) {
+    for (int n = 0, k = k_first; n < c.ke - c.kb; ++n, k += REV ? -1 : 1, idx += pstep) {
         Bundle nxt;
         if (PF) {
-            if (k + 1 < c.ke) nxt = issue(k + 1, idx + g.ps);
+            if (n + 1 < c.ke - c.kb) nxt = issue(REV ? k - 1 : k + 1, idx + pstep);
         } else {
             cur = issue(k, idx);
         }
@@ -779,8 +791,9 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         double right = __shfl_down(pc.x, 1, 64);
         if (c.lane == 0) left = cur.el;
         if (c.lane == 63) right = E1 ? cur.el : cur.er;
-        const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
-        const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
+        const double2 zm = REV ? pp : pm, zp = REV ? pm : pp;
+        const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, zm.x, zp.x);
+        const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, zm.y, zp.y);
         double2 rn;
         rn.x = c.in0 ? cur.rr.x + malpha * Ap0 : cur.rr.x;
         rn.y = c.in1 ? cur.rr.y + malpha * Ap1 : cur.rr.y;

@@ -28,6 +28,17 @@ struct BArgs {
 template <int TY, bool DIST, int FL>
 static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BArgs& a, int it) {
     const unsigned nb = (unsigned)(sg.tiles_x * sg.tiles_y * sg.tiles_z);
+    // sweep B marches z downwards on one device in 3-D (r03: it starts on the
+    // planes sweep A touched last, in the Infinity Cache; 512^3 sweep B
+    // 0.551 -> 0.539 ms, CG iteration 1.355 -> 1.335 ms, profiles/r03_rev.jsonl);
+    // CFD_HIP_CGB_REV=0 restores the upward march
+    static const bool rev = !(getenv("CFD_HIP_CGB_REV") && atoi(getenv("CFD_HIP_CGB_REV")) == 0);
+    if (!DIST && rev && c->geo.sz && sg.kmode == 0) {
+        hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, true>), dim3(nb), dim3(64 * TY), 0, c->stream,
+                              c->ta, c->tb, 0, sg, L, a.p, a.r, c->st, c->partials, c->counter,
+                              it, c->dsum, mbox(c));
+        return;
+    }
     hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL>), dim3(nb), dim3(64 * TY), 0, c->stream, c->ta,
                           c->tb, 0, sg, L, a.p, a.r, c->st, c->partials, c->counter, it,
                           c->dsum, mbox(c));
