@@ -2341,7 +2341,7 @@ struct Rb1Lds {
 
 // The body of k_rb1 for the tile width TC; bid = this workgroup's tile-block
 // index within its geometry g (k_rb1m runs two geometries in one grid).
-template <int FL, int TC, bool PF, bool DIST>
+template <int FL, int TC, bool PF, bool DIST, bool REV = false>
 __device__ __forceinline__ void rb1_body(
     Rb1Lds& L, int bid, SGeo g, RelaxCoef rc, const double* __restrict__ X,
     double* __restrict__ Y, const double* __restrict__ rhs, RxState* st, double* partials,
@@ -2448,17 +2448,26 @@ __device__ __forceinline__ void rb1_body(
     // a full step of latency hiding, and no register copy of a loaded value
     // (a copy would wait for the load). Without PF the loads are issued at
     // the end of step q and the three X planes shift through xm, xc, xp.
+    // REV (r03, one device): the march runs z downwards, D = -1: step q forms
+    // R_{q-1} and updates plane q, "ahead" is q - 1. Every cell's operands
+    // keep their z roles (z- / z+ are picked by direction), R depends on X
+    // only and the second colour on R only, and the residual is a max, so Y
+    // and the iteration's decision are bitwise the upward march's. The host
+    // alternates the direction per iteration, so each sweep starts on the
+    // planes the previous one wrote last (in the Infinity Cache).
+    constexpr int D = REV ? -1 : 1;
+    const int q0 = REV ? ke + 1 : kb - 2;  // the first step
     double2 xr[4], br[2], rm;
     double bmh, rmmh;
-    xr[0] = ldx(kb - 2);
-    xr[1] = ldx(kb - 1);
-    xr[2] = ldx(kb);
+    xr[0] = ldx(q0);
+    xr[1] = ldx(q0 + D);
+    xr[2] = ldx(q0 + 2 * D);
     xr[3] = zero;
-    br[0] = ldr(kb - 1);
+    br[0] = ldr(q0 + D);
     br[1] = zero;
     rm = zero;
     bmh = rmmh = 0.0;
-    lput(xb, (kb - 1) & 1, r, c, xr[1]);
+    lput(xb, (q0 + D) & 1, r, c, xr[1]);
     double m = 0.0;
     // E: cell i0 of the pair is the cell both updates of this step touch (the
     // first colour, (i+j+k) odd, of plane q+1 and the second of plane q)
@@ -2468,12 +2477,14 @@ __device__ __forceinline__ void rb1_body(
         constexpr int IM = P & 3, IC = (P + 1) & 3, IP = (P + 2) & 3, IN = (P + 3) & 3;
         constexpr int BQ = P & 1, BN = (P + 1) & 1;
         if constexpr (PF) {
-            xr[IN] = ldx(q + 3);
-            br[BN] = ldr(q + 2);
+            xr[IN] = ldx(q + 3 * D);
+            br[BN] = ldr(q + 2 * D);
         }
-        const double2 xm = xr[IM], xc = xr[IC], xp = xr[IP], bq = br[BQ];
+        // behind / centre / ahead of plane qa, then its z- / z+ neighbours
+        const double2 xbh = xr[IM], xc = xr[IC], xah = xr[IP], bq = br[BQ];
+        const double2 xm = REV ? xah : xbh, xp = REV ? xbh : xah;
         __syncthreads();
-        const int qa = q + 1;
+        const int qa = q + D;
         const bool qin = (qa >= g.k0 && qa < g.k1);
         const bool rin = qin && qa >= kb && qa < ke;
         // the output's LDS operands (R_q rows) are read up front, so one LDS
@@ -2506,13 +2517,16 @@ __device__ __forceinline__ void rb1_body(
             }
         }
         // ---- second colour of plane q from R_{q-1}, R_q, R_{q+1} ----
-        if (q >= kb && wo) {
+        // (rmmh: R behind, R: R ahead; REV swaps their z roles)
+        if ((REV ? q < ke : q >= kb) && wo) {
             double2 out = rm;
             if (E) {
-                const double v = sor1(rc, DivC{}, rm.x, rlr, rm.y, rys.x, ryn.x, rmmh, R.x, bmh);
+                const double rzm = REV ? R.x : rmmh, rzp = REV ? rmmh : R.x;
+                const double v = sor1(rc, DivC{}, rm.x, rlr, rm.y, rys.x, ryn.x, rzm, rzp, bmh);
                 if (own && in0) out.x = v;
             } else {
-                const double v = sor1(rc, DivC{}, rm.y, rm.x, rlr, rys.y, ryn.y, rmmh, R.y, bmh);
+                const double rzm = REV ? R.y : rmmh, rzp = REV ? rmmh : R.y;
+                const double v = sor1(rc, DivC{}, rm.y, rm.x, rlr, rys.y, ryn.y, rzm, rzp, bmh);
                 if (own && in1) out.y = v;
             }
             if (neu) {
@@ -2549,45 +2563,47 @@ __device__ __forceinline__ void rb1_body(
                 st2v<FL>(Y, (long long)q * g.ps + col, out);
             }
         }
-        // step q + 1 updates the .x cell iff this step did not
+        // step q + D updates the .x cell iff this step did not
         rmmh = E ? rm.y : rm.x;
         rm = R;
         bmh = E ? bq.y : bq.x;
         if constexpr (!PF) {
             xr[0] = xc;
-            xr[1] = xp;
-            xr[2] = ldx(q + 3);
-            br[0] = ldr(q + 2);
+            xr[1] = xah;
+            xr[2] = ldx(q + 3 * D);
+            br[0] = ldr(q + 2 * D);
         }
         // publish X_{q+2} and R_{q+1} for step q + 1 (their buffers were last
         // read in step q - 1, before this step's barrier)
-        lput(xb, (q + 2) & 1, r, c, xp);
-        lput(rb, (q + 1) & 1, r, c, rm);
+        lput(xb, (q + 2 * D) & 1, r, c, xah);
+        lput(rb, (q + D) & 1, r, c, rm);
     };
     // E(q) for the lane's row: ((j + q + kofs) & 1) == 0; E(kb - 2) == E(kb);
     // rows r and r + 16 h share the parity, so E is wave-uniform
-    const bool E0 = __builtin_amdgcn_readfirstlane(((j + kb + g.kofs) & 1) == 0 ? 1 : 0) != 0;
-    int q = kb - 2;
+    const bool E0 = __builtin_amdgcn_readfirstlane(((j + q0 + g.kofs) & 1) == 0 ? 1 : 0) != 0;
+    // steps q0, q0 + D, ...: ke - kb + 2 of them (R is formed one plane ahead)
+    const int nsteps = ke - kb + 2;
+    int n = 0;
     auto march = [&](auto E0c) __attribute__((always_inline)) {
         constexpr bool A = decltype(E0c)::value;
         using TA = BoolC<A>;
         using TB = BoolC<!A>;
         if constexpr (PF) {
-            for (; q + 3 < ke; q += 4) {
-                step(TA{}, IntC<0>{}, q);
-                step(TB{}, IntC<1>{}, q + 1);
-                step(TA{}, IntC<2>{}, q + 2);
-                step(TB{}, IntC<3>{}, q + 3);
+            for (; n + 3 < nsteps; n += 4) {
+                step(TA{}, IntC<0>{}, q0 + D * n);
+                step(TB{}, IntC<1>{}, q0 + D * (n + 1));
+                step(TA{}, IntC<2>{}, q0 + D * (n + 2));
+                step(TB{}, IntC<3>{}, q0 + D * (n + 3));
             }
-            if (q < ke) step(TA{}, IntC<0>{}, q);
-            if (q + 1 < ke) step(TB{}, IntC<1>{}, q + 1);
-            if (q + 2 < ke) step(TA{}, IntC<2>{}, q + 2);
+            if (n < nsteps) step(TA{}, IntC<0>{}, q0 + D * n);
+            if (n + 1 < nsteps) step(TB{}, IntC<1>{}, q0 + D * (n + 1));
+            if (n + 2 < nsteps) step(TA{}, IntC<2>{}, q0 + D * (n + 2));
         } else {
-            for (; q + 1 < ke; q += 2) {
-                step(TA{}, IntC<0>{}, q);
-                step(TB{}, IntC<0>{}, q + 1);
+            for (; n + 1 < nsteps; n += 2) {
+                step(TA{}, IntC<0>{}, q0 + D * n);
+                step(TB{}, IntC<0>{}, q0 + D * (n + 1));
             }
-            if (q < ke) step(TA{}, IntC<0>{}, q);
+            if (n < nsteps) step(TA{}, IntC<0>{}, q0 + D * n);
         }
     };
     if (E0) march(BoolC<true>{});
@@ -2637,14 +2653,14 @@ __device__ __forceinline__ void rb1_body(
     }
 }
 
-template <int FL, int TC, bool PF, bool DIST = false>
+template <int FL, int TC, bool PF, bool DIST = false, bool REV = false>
 static __global__ __launch_bounds__(1024, 4) void k_rb1(
     SGeo g, RelaxCoef rc, const double* __restrict__ X, double* __restrict__ Y,
     const double* __restrict__ rhs, RxState* st, double* partials, unsigned* counter, int it,
     const double* __restrict__ RH, int rh_lo, int rh_hi, Mbox* mb, unsigned long long* dred,
     int neu) {
     __shared__ Rb1Lds L;
-    rb1_body<FL, TC, PF, DIST>(L, blockIdx.x, g, rc, X, Y, rhs, st, partials, counter, it, RH,
+    rb1_body<FL, TC, PF, DIST, REV>(L, blockIdx.x, g, rc, X, Y, rhs, st, partials, counter, it, RH,
                                rh_lo, rh_hi, mb, dred, neu);
 }
 
@@ -2655,18 +2671,19 @@ static __global__ __launch_bounds__(1024, 4) void k_rb1(
 // of 124); the strip's TC-16 / TC-32 tiles are 60 / 28 rows tall, so the
 // column strip needs 4.8x / 2.2x fewer workgroups. Both geometries share the
 // grid-wide residual reduction (part_total 0: gridDim.x workgroups).
-template <int FL, int TC2>
+template <int FL, int TC2, bool REV = false>
 static __global__ __launch_bounds__(1024, 4) void k_rb1m(
     SGeo g64, SGeo g2, int nb64, RelaxCoef rc, const double* __restrict__ X,
     double* __restrict__ Y, const double* __restrict__ rhs, RxState* st, double* partials,
     unsigned* counter, int it, int neu) {
     __shared__ Rb1Lds L;
     if ((int)blockIdx.x < nb64)
-        rb1_body<FL, 64, true, false>(L, blockIdx.x, g64, rc, X, Y, rhs, st, partials, counter,
-                                      it, nullptr, 0, 0, nullptr, nullptr, neu);
+        rb1_body<FL, 64, true, false, REV>(L, blockIdx.x, g64, rc, X, Y, rhs, st, partials,
+                                           counter, it, nullptr, 0, 0, nullptr, nullptr, neu);
     else
-        rb1_body<FL, TC2, true, false>(L, blockIdx.x - nb64, g2, rc, X, Y, rhs, st, partials,
-                                       counter, it, nullptr, 0, 0, nullptr, nullptr, neu);
+        rb1_body<FL, TC2, true, false, REV>(L, blockIdx.x - nb64, g2, rc, X, Y, rhs, st,
+                                            partials, counter, it, nullptr, 0, 0, nullptr,
+                                            nullptr, neu);
 }
 
 // R (the first colour SOR-updated, linear_solver_redblack.c:97-114) of a

@@ -556,13 +556,14 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
             // of Y and plain rhs loads (r03: the NT rhs loads of 15 made the
             // neighbouring tiles re-fetch the rhs halo rows; 512^3 0.744 ->
             // 0.726 ms, 1024^2 x 512 2.925 -> 2.85 ms, fetch 19.6 -> 18.7
-            // B/cell, profiles/r03_rbfl.jsonl); CFD_HIP_RB1_FL = 12 / 14 / 15
-            // select the other hint sets (A/B)
-            static const int rb1_fl = [] {
-                const char* e = getenv("CFD_HIP_RB1_FL");
-                const int v = e ? atoi(e) : FLR;
-                return (v == 12 || v == 14 || v == 15) ? v : FLR;
-            }();
+            // B/cell, profiles/r03_rbfl.jsonl)
+            // odd iterations march z downwards (REV), so each sweep starts on
+            // the planes the previous one wrote last, in the Infinity Cache;
+            // bitwise either way (kernels.hpp rb1_body). CFD_HIP_RB1_ALT=0:
+            // every iteration upwards
+            static const bool rb1_alt = !(getenv("CFD_HIP_RB1_ALT") &&
+                                          atoi(getenv("CFD_HIP_RB1_ALT")) == 0);
+            const bool rev = rb1_alt && rb1_pf && (it & 1);
 #define RB1_LAUNCH(TCV, PFV)                                                                   \
     hipExtLaunchKernelGGL((k_rb1<FLR, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
                           c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
@@ -580,27 +581,20 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                                               c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs, c->rxst,
                                               c->partials, c->counter, it, neu_fold ? 1 : 0);
                     };
-                    if (rb1_fl == 12) go(k_rb1m<12, 16>);
-                    else if (rb1_fl == 14) go(k_rb1m<14, 16>);
-                    else if (rb1_fl == 15) go(k_rb1m<15, 16>);
+                    if (rev) go(k_rb1m<FLR, 16, true>);
                     else go(k_rb1m<FLR, 16>);
                 }, it);
             } else
             timed(c, HIP_KT_RELAX, [&] {
-                auto go = [&](auto kern) {
-                    hipExtLaunchKernelGGL(kern, dim3(nb1), dim3(1024), 0, c->stream, c->ta, c->tb,
-                                          0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,
-                                          c->counter, it, (const double*)nullptr, 0, 0,
-                                          (Mbox*)nullptr, (unsigned long long*)nullptr,
-                                          neu_fold ? 1 : 0);
-                };
-                if (rb1_pf && c->rb1_tc == 64 && rb1_fl != FLR) {
-                    if (rb1_fl == 12) go(k_rb1<12, 64, true>);
-                    else if (rb1_fl == 14) go(k_rb1<14, 64, true>);
-                    else go(k_rb1<15, 64, true>);
-                } else if (!rb1_pf) RB1_LAUNCH(64, false);
+                if (!rb1_pf) RB1_LAUNCH(64, false);
                 else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
                 else if (c->rb1_tc == 16) RB1_LAUNCH(16, true);
+                else if (rev)
+                    hipExtLaunchKernelGGL((k_rb1<FLR, 64, true, false, true>), dim3(nb1),
+                                          dim3(1024), 0, c->stream, c->ta, c->tb, 0, c->rgeo, rc,
+                                          xi, xo, c->rhs, c->rxst, c->partials, c->counter, it,
+                                          (const double*)nullptr, 0, 0, (Mbox*)nullptr,
+                                          (unsigned long long*)nullptr, neu_fold ? 1 : 0);
                 else RB1_LAUNCH(64, true);
             });
 #undef RB1_LAUNCH
