@@ -1,0 +1,48 @@
+#!/bin/bash
+# One-box A/B of an environment switch -- the form of every experiment
+# recorded in profiles/ (their notes give the switch, values and command).
+#   SW      the variable (e.g. CFD_HIP_CGB_REV; CFD_AMD_HIP_LIB selects another
+#           build of libcfd_hip.so); a value "-" leaves it unset
+#   VALUES  the values, in the order they run in each round
+#   TESTS   pytest files run under every value before timing (parity first)
+#   CMD     the measuring command; each JSON line it prints is tagged with
+#           {"<SW>": value, "round": r}
+#   ROUNDS  interleaved rounds (default 2)
+#   PMC     optional counters: one rocprofv3 --pmc pass per counter and value
+#           over PMC_CMD (default CMD), summarised by tools/pmc_kernels.py
+# Output: gpurun_out/<TAG>/{pytest_<v>.log, ab.jsonl, pmc.jsonl}.
+# usage: TAG=rev SW=CFD_HIP_CGB_REV VALUES="0 1" TESTS="tests/test_gpu_parity.py" \
+#        CMD="python3 tools/relax_bench.py" tools/ab.sh
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-ab}
+O=gpurun_out/$TAG
+mkdir -p $O
+: "${SW:?SW (the environment switch) is required}" "${CMD:?CMD is required}"
+VALUES=${VALUES:-"0 1"}
+run() {  # run <value> <command...>: the command with SW set to value (or unset)
+  local v=$1; shift
+  if [ "$v" = "-" ]; then env -u "$SW" "$@"; else env "$SW=$v" "$@"; fi
+}
+if [ -n "$TESTS" ]; then
+  for v in $VALUES; do
+    run "$v" timeout -k 10 ${TEST_TIMEOUT:-500} python3 -u -m pytest $TESTS -x -q --timeout 300 \
+        --timeout-method thread > $O/pytest_$v.log 2>&1
+    rc=$?; echo "pytest $SW=$v exit $rc"; tail -1 $O/pytest_$v.log; [ $rc -ne 0 ] && exit $rc
+  done
+fi
+for round in $(seq 1 ${ROUNDS:-2}); do
+  for v in $VALUES; do
+    run "$v" timeout -k 10 ${CMD_TIMEOUT:-300} $CMD > $O/cmd.out 2> $O/cmd.err || { tail -5 $O/cmd.err; exit 1; }
+    sed "s/^{/{\"$SW\": \"$v\", \"round\": $round, /" $O/cmd.out >> $O/ab.jsonl
+  done
+done
+cat $O/ab.jsonl
+for v in $VALUES; do
+  for ctr in $PMC; do
+    run "$v" timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $ctr -d $O/pmc_${v}_$ctr -o p \
+        --output-format csv -- ${PMC_CMD:-$CMD} > /dev/null 2>&1 || exit $?
+    python3 tools/pmc_kernels.py $O/pmc_${v}_$ctr --note "$SW=$v $ctr" >> $O/pmc.jsonl
+  done
+done
+exit 0
