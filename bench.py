@@ -86,9 +86,11 @@ def parse():
                     help="seconds allowed for the CPU baseline child process")
     ap.add_argument("--kchunk", type=int, default=0)
     ap.add_argument("--sweep-rows", type=int, default=16)
-    ap.add_argument("--sweep-variant", type=int, default=15,
-                    help="CG sweep variant: bit0 NT stores, bit1 NT loads, bit2 plane prefetch "
-                         "(built: 0-4, 7)")
+    ap.add_argument("--sweep-variant", type=int,
+                    default=int(os.environ.get("CFD_BENCH_SWEEP_VARIANT", "15")),
+                    help="CG sweep variant: bit0 NT stores, bit1 NT loads, bit2 plane prefetch, "
+                         "bit3 one edge load (built: 0-4, 7, 15, and 23 / 31 with 16 rows; "
+                         "default 15, or CFD_BENCH_SWEEP_VARIANT)")
     ap.add_argument("--cg-variant", type=int, default=0, choices=(0, 1),
                     help="0: textbook CG (the reference's loop); 1: single-reduction "
                          "(Chronopoulos-Gear) CG")
