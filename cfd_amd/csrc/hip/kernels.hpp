@@ -2367,8 +2367,11 @@ __device__ __forceinline__ void rb1_body(
         a[p][r][1][l] = v.y;
     };
     if (st->done) return;
-    const int nt = g.tiles_x * g.tiles_y * g.tiles_z;
-    const int t = xcd_tile(bid, nt);
+    // tile = block index: round-robin dispatch spreads consecutive tiles over
+    // the eight XCDs (r03: faster here than xcd_tile's contiguous ranges,
+    // 2.86-2.87 -> 2.82-2.83 ms per iteration at 1024^2 x 512, equal at 512^3,
+    // profiles/r03_tile_order.jsonl)
+    const int t = bid;
     const int tx = t % g.tiles_x;
     const int rest = t / g.tiles_x;
     const int ty = rest % g.tiles_y;

@@ -20,6 +20,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 : "${SW:?SW (the environment switch) is required}" "${CMD:?CMD is required}"
 VALUES=${VALUES:-"0 1"}
+safe() { echo "$1" | tr -c 'A-Za-z0-9_.\n-' '_'; }  # a value as a file-name part
 run() {  # run <value> <command...>: the command with SW set to value (or unset)
   local v=$1; shift
   if [ "$v" = "-" ]; then env -u "$SW" "$@"; else env "$SW=$v" "$@"; fi
@@ -27,22 +28,23 @@ run() {  # run <value> <command...>: the command with SW set to value (or unset)
 if [ -n "$TESTS" ]; then
   for v in $VALUES; do
     run "$v" timeout -k 10 ${TEST_TIMEOUT:-500} python3 -u -m pytest $TESTS -x -q --timeout 300 \
-        --timeout-method thread > $O/pytest_$v.log 2>&1
-    rc=$?; echo "pytest $SW=$v exit $rc"; tail -1 $O/pytest_$v.log; [ $rc -ne 0 ] && exit $rc
+        --timeout-method thread > $O/pytest_$(safe "$v").log 2>&1
+    rc=$?; echo "pytest $SW=$v exit $rc"; tail -1 $O/pytest_$(safe "$v").log; [ $rc -ne 0 ] && exit $rc
   done
 fi
 for round in $(seq 1 ${ROUNDS:-2}); do
   for v in $VALUES; do
     run "$v" timeout -k 10 ${CMD_TIMEOUT:-300} $CMD > $O/cmd.out 2> $O/cmd.err || { tail -5 $O/cmd.err; exit 1; }
-    sed "s/^{/{\"$SW\": \"$v\", \"round\": $round, /" $O/cmd.out >> $O/ab.jsonl
+    sed "s|^{|{\"$SW\": \"$v\", \"round\": $round, |" $O/cmd.out >> $O/ab.jsonl || exit 1
   done
 done
 cat $O/ab.jsonl
 for v in $VALUES; do
   for ctr in $PMC; do
-    run "$v" timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $ctr -d $O/pmc_${v}_$ctr -o p \
+    d=$O/pmc_$(safe "$v")_$ctr
+    run "$v" timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $ctr -d $d -o p \
         --output-format csv -- ${PMC_CMD:-$CMD} > /dev/null 2>&1 || exit $?
-    python3 tools/pmc_kernels.py $O/pmc_${v}_$ctr --note "$SW=$v $ctr" >> $O/pmc.jsonl
+    python3 tools/pmc_kernels.py $d --note "$SW=$v $ctr" >> $O/pmc.jsonl
   done
 done
 exit 0
