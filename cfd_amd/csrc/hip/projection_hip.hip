@@ -1005,7 +1005,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             // TC-32 strips (R in 29..60) measured slower (1024^2 x 512: 2.96 vs
             // 2.93 ms); TC-16 ones faster (512^3: 0.734 vs 0.760 ms,
             // profiles/r03_rb1_strip.jsonl)
-            const int stc = (R == 0) ? 0 : (R <= 28 ? 16 : 0);
+            // R = 1 (nx = 124 T + 1): the T full tiles already store every
+            // pair (cell nx - 1 is the Neumann mirror), so no strip
+            const int stc = (R >= 2 && R <= 28) ? 16 : 0;
             if (stc) {
                 c->rb_strip_tc = stc;
                 SGeo& m = c->rg_main;
@@ -1796,8 +1798,14 @@ static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
             double* host[5];
             double* dev[5];
             const int nf = host_fields(c, f, host, dev);
-            if (full_up || !c->hash_ok || c->hash_nf != nf) ctx_host_hash(c, host, nf, false, c->host_hash);
-            ctx_host_hash(c, host, nf, true, c->host_hash1);
+            if (full_up || !c->hash_ok || c->hash_nf != nf) {
+                ctx_host_hash(c, host, nf, false, c->host_hash);
+                ctx_host_hash(c, host, nf, true, c->host_hash1);
+            } else if (c->res_steps % verify == 0) {
+                // layer 1 changes with every shell download: its reference is
+                // retaken only before a step that checks (the next one)
+                ctx_host_hash(c, host, nf, true, c->host_hash1);
+            }
             c->hash_nf = nf;
             c->hash_ok = 1;
         }

@@ -252,8 +252,18 @@ void ctx_host_hash(const hip_proj_ctx* c, const double* const* host, int nf, boo
         if (nt == 1) {
             work(0);
         } else {
+            // reached from extern "C" entry points: a thread that cannot be
+            // created (std::system_error) must not cross the C ABI, so its
+            // share runs on this thread instead (the sum is order-free)
             std::vector<std::thread> th;
-            for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+            th.reserve(nt);
+            for (int t = 0; t < nt; ++t) {
+                try {
+                    th.emplace_back(work, t);
+                } catch (...) {
+                    work(t);
+                }
+            }
             for (auto& t : th) t.join();
         }
         unsigned long long h = 0;

@@ -107,11 +107,15 @@ typedef struct {
     int dirty_verify_interval;    /* resident mode guard: every N-th resident step first
                                      checks that the caller left the interior of its host
                                      arrays (every cell but the outer layer) as the last
-                                     step did (a 64-bit position-weighted hash, two
-                                     multithreaded host passes every N steps). A changed
-                                     interior fails the step with CFD_ERROR_INVALID before
-                                     anything runs; the device state is kept. 0 = off
-                                     (default). */
+                                     step did (64-bit position-weighted hashes: per N
+                                     steps, two multithreaded host passes at the checked
+                                     step and one over the layer next to the boundary
+                                     after the step before it). A changed interior fails
+                                     the checked step with CFD_ERROR_INVALID before
+                                     anything runs; the device state is kept. With N > 1
+                                     a write is found up to N-1 steps after it was made,
+                                     and those steps have run on the device's state.
+                                     0 = off (default). */
 } hip_proj_config_t;
 
 typedef struct hip_proj_ctx hip_proj_ctx_t;

@@ -93,6 +93,10 @@ def main():
                       f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
                       f"OMP_PLACES={os.environ.get('OMP_PLACES')}); sample wall {wall:.1f} s"),
            "cg_iter_ms": round(t_cg_iter * 1e3, 2),
+           # timed CG iterations -> the GPU's iterations per step (the factor
+           # the sampled CG time is multiplied by)
+           "scale_factor": round(a.k_gpu / max(it, 1), 3),
+           "cg_iters_timed": it,
            "cg_iter_GBps_80": round(80.0 * n_int / t_cg_iter / 1e9, 2),
            "status": s,
            "host_cpu_model": host_cpu_model(), "host_cpus": os.cpu_count(),

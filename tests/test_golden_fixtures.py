@@ -85,3 +85,37 @@ def test_cavity128_re1000_fixture_consistent():
         assert s == A.CFD_SUCCESS
         its.append(it)
     assert its == list(snap["iters"][:10])
+
+
+@pytest.mark.parametrize("name,threads", [("conv32cap", 1), ("conv32cap", 3)])
+def test_convection_fixture_regenerates_bitwise(name, threads):
+    """convection_conv32cap.json (configs[4] at tol 1e-6, cap 20000: step 2
+    runs 20001 RB-SOR iterations) from the oracle at 1 and 3 threads: the
+    fingerprints do not depend on the thread count (the fixtures were written
+    with 8)."""
+    import hashlib
+
+    import bench
+
+    fx = json.loads((GOLD / f"convection_{name}.json").read_text())
+    nx, ny, nz = fx["grid"]
+    g, p, T0 = bench.convection_setup(nx, ny, nz)
+    f = api.FlowField(nx, ny, nz)
+    f.u[...] = f.v[...] = f.w[...] = f.p[...] = 0.0
+    f.rho[...] = 1.0
+    f.T[...] = np.broadcast_to(T0[None, None, :], f.T.shape)
+    oracle.set_threads(threads)
+    oracle.set_projection_poisson_params(oracle.poisson_params(
+        tolerance=fx["tolerance"], max_iterations=fx["max_iterations"]))
+    try:
+        for want in fx["steps"]:
+            s, _, it = oracle.projection_step(f, g, p, A.ORACLE_POISSON_REDBLACK)
+            ps = oracle.last_poisson_stats()
+            assert (s, ps.iterations, ps.final_residual) == (
+                want["status"], want["iterations"], want["final_residual"])
+            for k, w in want["fields"].items():
+                a = np.ascontiguousarray(getattr(f, k))
+                assert hashlib.sha256(a.tobytes()).hexdigest() == w["sha256"], k
+    finally:
+        oracle.set_projection_poisson_params(None)
+        oracle.set_threads(1)

@@ -21,6 +21,9 @@ pytestmark = pytest.mark.gpu
     ((126, 14, 5), dict(max_iterations=30, check_interval=2)),
     ((255, 50, 140), dict(max_iterations=6)),
     ((63, 70, 12), dict(max_iterations=9)),
+    # nx = 124 T + 1: no remainder strip (the full tiles store every pair)
+    ((249, 21, 10), dict(max_iterations=11)),
+    ((250, 21, 10), dict(max_iterations=11)),
 ])
 @pytest.mark.parametrize("tc", ["64", "32", "16"])
 def test_rb_one_pass_bitwise(hip_lib, shape, kw, tc, monkeypatch):
