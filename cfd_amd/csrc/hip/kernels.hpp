@@ -2011,6 +2011,11 @@ static __global__ __launch_bounds__(NT) void k_residual_linf(Geo g, ResCoef rc,
 struct RxState {
     double tol, abs_tol, rel_tol, res0, res;
     int iterations, done, status, max_iter, check_interval, result;  // result: buffer index
+    // two iterations per sweep (k_rb2, rb2.hpp): the iterate index the loop
+    // stopped on, whether `res` is that iterate's exact residual, the
+    // host-resolved exact residual of iterate ovr_it (-1: none), and max |rhs|
+    int res_it, res_exact, ovr_it, pad0;
+    double ovr_m, bmax;
 };
 
 constexpr int RX_RED = 0;
@@ -2030,6 +2035,7 @@ __device__ __forceinline__ void rx_finish(RxState* st, double m, int it) {
             st->status = ST_CONVERGED;
             st->iterations = 0;
             st->result = 0;
+            st->res_it = 0;
         }
         return;
     }
@@ -2041,6 +2047,7 @@ __device__ __forceinline__ void rx_finish(RxState* st, double m, int it) {
             st->status = ST_CONVERGED;
             st->iterations = it;  // iter + 1 at the break
             st->result = it & 1;
+            st->res_it = it;
             return;
         }
     }
@@ -2049,6 +2056,7 @@ __device__ __forceinline__ void rx_finish(RxState* st, double m, int it) {
         st->status = ST_MAX_ITER;
         st->iterations = st->max_iter + 1;
         st->result = it & 1;
+        st->res_it = it;
     }
 }
 
@@ -2065,6 +2073,12 @@ static __global__ void k_rx_init(RxState* st, double rel_tol, double abs_tol, in
         st->max_iter = max_iter;
         st->check_interval = check_interval;
         st->result = 0;
+        st->res_it = 0;
+        st->res_exact = 1;
+        st->ovr_it = -1;
+        st->pad0 = 0;
+        st->ovr_m = 0.0;
+        st->bmax = 0.0;
     }
 }
 

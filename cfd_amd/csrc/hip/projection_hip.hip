@@ -10,6 +10,7 @@
 // is no host round trip per iteration (the reference GPU path does two per
 // iteration, poisson_cg_gpu_solve.cuh:189-203).
 #include "ctx.hpp"
+#include "rb2.hpp"
 
 template <int TY, bool FIRST, bool DIST, int FL, bool FOLD>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
@@ -413,6 +414,234 @@ static cfd_status_t residual_linf(hip_proj_ctx* c, const double* x, const ResCoe
 static cfd_status_t ensure_aux(hip_proj_ctx* c, bool need_rhs, bool need_xt);
 static_assert(sizeof(RxState) <= sizeof(CgState), "RxState polls through the CgState slots");
 
+// One k_rb1 sweep on one device (3-D): xi -> xo (one RB-SOR iteration with
+// its Neumann shell when neu_fold), the L-inf residual of xi decided on `st`
+// as sweep `it` of the fused loop.
+static void rb1_sweep_single(hip_proj_ctx* c, const RelaxCoef& rc, const double* xi, double* xo,
+                             int it, RxState* st, bool neu_fold) {
+    constexpr int FLR = SW_NT_STORE | SW_PREFETCH | SW_EDGE1;
+    const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
+    // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the
+    // end-of-step loads (experiments)
+    static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
+                                 atoi(getenv("CFD_HIP_RB1_PF")) == 0);
+    // memory hints of k_rb1 / k_rb1m (SW_* bits): FLR = 13, NT stores
+    // of Y and plain rhs loads (r03: the NT rhs loads of 15 made the
+    // neighbouring tiles re-fetch the rhs halo rows; 512^3 0.744 ->
+    // 0.726 ms, 1024^2 x 512 2.925 -> 2.85 ms, fetch 19.6 -> 18.7
+    // B/cell, profiles/r03_rbfl.jsonl)
+    // odd iterations march z downwards (REV), so each sweep starts on
+    // the planes the previous one wrote last, in the Infinity Cache;
+    // bitwise either way (kernels.hpp rb1_body). CFD_HIP_RB1_ALT=0:
+    // every iteration upwards
+    static const bool rb1_alt = !(getenv("CFD_HIP_RB1_ALT") &&
+                                  atoi(getenv("CFD_HIP_RB1_ALT")) == 0);
+    const bool rev = rb1_alt && rb1_pf && (it & 1);
+#define RB1_LAUNCH(TCV, PFV)                                                                   \
+    hipExtLaunchKernelGGL((k_rb1<FLR, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
+                          c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, st, c->partials,            \
+                          c->counter, it, (const double*)nullptr, 0, 0, (Mbox*)nullptr,      \
+                          (unsigned long long*)nullptr, neu_fold ? 1 : 0)
+    if (c->rb_strip_tc && rb1_pf) {
+        // full-width tiles and the narrow strip in one grid
+        const SGeo& gm = c->rg_main;
+        const SGeo& gs = c->rg_strip;
+        const int nbm = gm.tiles_x * gm.tiles_y * gm.tiles_z;
+        const unsigned nbt = (unsigned)(nbm + gs.tiles_x * gs.tiles_y * gs.tiles_z);
+        timed(c, HIP_KT_RELAX, [&] {
+            auto go = [&](auto kern) {
+                hipExtLaunchKernelGGL(kern, dim3(nbt), dim3(1024), 0, c->stream, c->ta,
+                                      c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs, st,
+                                      c->partials, c->counter, it, neu_fold ? 1 : 0);
+            };
+            if (rev) go(k_rb1m<FLR, 16, true>);
+            else go(k_rb1m<FLR, 16>);
+        }, it);
+    } else
+    timed(c, HIP_KT_RELAX, [&] {
+        if (!rb1_pf) RB1_LAUNCH(64, false);
+        else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
+        else if (c->rb1_tc == 16) RB1_LAUNCH(16, true);
+        else if (rev)
+            hipExtLaunchKernelGGL((k_rb1<FLR, 64, true, false, true>), dim3(nb1),
+                                  dim3(1024), 0, c->stream, c->ta, c->tb, 0, c->rgeo, rc,
+                                  xi, xo, c->rhs, st, c->partials, c->counter, it,
+                                  (const double*)nullptr, 0, 0, (Mbox*)nullptr,
+                                  (unsigned long long*)nullptr, neu_fold ? 1 : 0);
+        else RB1_LAUNCH(64, true);
+    });
+#undef RB1_LAUNCH
+}
+
+
+// Two RB-SOR iterations per sweep (k_rb2, rb2.hpp) on one device in 3-D with
+// the Neumann shell, check_interval 1 (the reference default): the fused
+// loop of relax_solve_fused with sweep 0 a k_rb1 sweep (the exact initial
+// residual), then k_rb2 sweeps s = 1, 3, 5, ... (iterate s -> s + 2, the
+// decisions on iterates s and s + 1). The host logs every launch (iterate,
+// kind, buffers), so after the loop stops it finds the decided iterate: the
+// input of a launch (intact) or the middle iterate of a k_rb2 sweep, which it
+// recomputes with one k_rb1 sweep from that sweep's input. With apx (the
+// product form) the device may also stop on
+//  - ST_RB2_AMBIG (an approximate residual within its bound of the
+//    threshold): the host computes that iterate's exact residual and resumes
+//    the loop from the iterate with it as an override;
+//  - ST_RB2_UNCERT (a value outside the certified range): the host resumes
+//    from that sweep's input with k_rb1 sweeps for the rest of the solve;
+// and the final residual is recomputed exactly. Iterates, iteration counts,
+// statuses and residuals are those of relax_solve_fused.
+static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double rel_tol,
+                                    double abs_tol, int max_iter, bool apx) {
+    ST_TRY(ensure_aux(c, true, true));
+    if (!c->rxst) HIP_TRY(hipMalloc((void**)&c->rxst, sizeof(RxState)));
+    if (!c->rxst2) HIP_TRY(hipMalloc((void**)&c->rxst2, sizeof(RxState)));
+    Rb2Coef cf;
+    cf.rc = rc;
+    cf.k2 = 2.0 * (rc.rdx2 + rc.rdy2 + rc.inv_dz2);
+    cf.kb = rc.rdx2 + rc.rdy2 + rc.inv_dz2;
+    cf.escale = 1.0;
+    cf.elim = -800.0;
+    if (const char* e = getenv("CFD_HIP_RB2_TEST")) {  // tests: force the host paths
+        const int v = atoi(e);
+        if (v == 1) cf.escale = 1e300;  // every approximate decision ambiguous
+        if (v == 2) cf.elim = 4096.0;   // every sweep uncertified
+    }
+    constexpr int FLR = SW_NT_STORE | SW_PREFETCH | SW_EDGE1;
+    const SGeo& g2 = c->r2geo;
+    const unsigned nb2 = (unsigned)(g2.tiles_x * g2.tiles_y * g2.tiles_z);
+    hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
+                          rel_tol, abs_tol, max_iter, 1);
+    if (apx) {
+        const int nbm = (int)std::min<long long>(4LL * c->grid_cap,
+                                                 ((long long)c->nx * c->ny * c->nz + 255) / 256);
+        hipExtLaunchKernelGGL(k_rb2_bmax, dim3(std::max(1, nbm)), dim3(256), 0, c->stream,
+                              c->ta, c->tb, 0, c->geo, (const double*)c->rhs, c->rxst);
+    }
+    struct Launch {
+        int s, kind;  // kind 1: k_rb1 (iterate s -> s + 1), 2: k_rb2 (s -> s + 2)
+        double *x, *y;
+    };
+    std::vector<Launch> log;
+    double* bx = c->pn;
+    double* by = c->xt;
+    int cur = 0;
+    bool exact_mode = false, force_certx = false;
+    auto launch = [&]() {
+        if (cur == 0 || exact_mode) {
+            rb1_sweep_single(c, rc, bx, by, cur, c->rxst, true);
+            log.push_back({cur, 1, bx, by});
+            cur += 1;
+        } else {
+            const int certx = (force_certx || log.empty() || log.back().kind == 1) ? 1 : 0;
+            force_certx = false;
+            timed(c, HIP_KT_RELAX, [&] {
+                if (apx)
+                    hipExtLaunchKernelGGL((k_rb2<true, FLR>), dim3(nb2), dim3(1024), 0, c->stream,
+                                          c->ta, c->tb, 0, g2, cf, (const double*)bx, by,
+                                          (const double*)c->rhs, c->rxst, c->partials,
+                                          c->counter, cur, certx);
+                else
+                    hipExtLaunchKernelGGL((k_rb2<false, FLR>), dim3(nb2), dim3(1024), 0,
+                                          c->stream, c->ta, c->tb, 0, g2, cf, (const double*)bx,
+                                          by, (const double*)c->rhs, c->rxst, c->partials,
+                                          c->counter, cur, certx);
+            }, cur);
+            log.push_back({cur, 2, bx, by});
+            cur += 2;
+        }
+        std::swap(bx, by);
+    };
+    // the middle iterate of k_rb2 launch L, recomputed into L.y (one k_rb1
+    // sweep on a scratch state that never decides)
+    auto recompute_mid = [&](const Launch& L) {
+        hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
+                              c->rxst2, 0.0, 0.0, 0x7fffffff, 1);
+        rb1_sweep_single(c, rc, L.x, L.y, 1, c->rxst2, true);
+    };
+    auto find = [&](int t, int* kind_mid) -> int {  // log index holding iterate t
+        for (int q = (int)log.size() - 1; q >= 0; --q) {
+            if (log[q].s == t) {
+                *kind_mid = 0;
+                return q;
+            }
+            if (log[q].kind == 2 && log[q].s + 1 == t) {
+                *kind_mid = 1;
+                return q;
+            }
+        }
+        return -1;
+    };
+    const ResCoef resc{rc.dx2, rc.dy2, rc.inv_dz2};
+    RxState* hs = reinterpret_cast<RxState*>(c->h_state);
+    for (;;) {
+        int chunk = 8, slot = 0, prev = -1;
+        const int chunk_max = std::max(1, c->cfg.poll_interval);
+        while (cur <= max_iter) {
+            const int target = cur + chunk;  // iterates launched this chunk
+            while (cur <= max_iter && cur < target) launch();
+            HIP_TRY(hipMemcpyAsync(&hs[slot], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost,
+                                   c->stream));
+            HIP_TRY(hipEventRecord(c->ev_poll[slot], c->stream));
+            if (prev >= 0) {
+                HIP_TRY(hipEventSynchronize(c->ev_poll[prev]));
+                if (hs[prev].done) break;
+            }
+            prev = slot;
+            slot ^= 1;
+            chunk = std::min(chunk * 2, chunk_max);
+        }
+        HIP_TRY(hipMemcpyAsync(&hs[2], c->rxst, sizeof(RxState), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        const RxState r = hs[2];
+        if (!r.done) {
+            set_err(CFD_ERROR, "relaxation (k_rb2): device loop ended without a decision");
+            return CFD_ERROR;
+        }
+        int mid = 0;
+        const int li = find(r.res_it, &mid);
+        if (li < 0) {
+            set_err(CFD_ERROR, "relaxation (k_rb2): decided iterate not in the launch log");
+            return CFD_ERROR;
+        }
+        const Launch L = log[li];
+        if (r.status == ST_RB2_UNCERT) {
+            // rerun from this sweep's input with k_rb1 sweeps
+            log.resize(li);
+            exact_mode = true;
+            bx = L.x;
+            by = L.y;
+            cur = L.s;
+            hipExtLaunchKernelGGL(k_rb2_resume, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb,
+                                  0, c->rxst, -1, 0.0);
+            continue;
+        }
+        double* xt = mid ? L.y : L.x;
+        if (mid) recompute_mid(L);
+        if (r.status == ST_RB2_AMBIG) {
+            double m = 0.0;
+            ST_TRY(residual_linf(c, xt, resc, &m));
+            log.resize(li);
+            force_certx = true;  // the next sweep's input came from a recompute
+            bx = xt;
+            by = mid ? L.x : L.y;
+            cur = r.res_it;
+            hipExtLaunchKernelGGL(k_rb2_resume, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb,
+                                  0, c->rxst, r.res_it, m);
+            continue;
+        }
+        flush_timing(c);
+        double res = r.res;
+        if (!r.res_exact) ST_TRY(residual_linf(c, xt, resc, &res));
+        if (xt != c->pn) std::swap(c->pn, c->xt);
+        c->pstats.initial_residual = r.res0;
+        c->pstats.iterations = r.iterations;
+        c->pstats.final_residual = res;
+        c->pstats.status = (poisson_solver_status_t)r.status;
+        return (r.status == ST_CONVERGED) ? CFD_SUCCESS : CFD_ERROR_MAX_ITER;
+    }
+}
+
 // Fused relaxation loop (single device, 16-row sweep tiles): the iteration's
 // sweeps, boundary shell and convergence test all run on the device (k_rx,
 // kernels.hpp); the host polls the state one chunk behind, like cg_solve.
@@ -474,6 +703,12 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     static const bool fold_env = !(getenv("CFD_HIP_RB1_FOLD") &&
                                    atoi(getenv("CFD_HIP_RB1_FOLD")) == 0);
     const bool neu_fold = single && fold_env && c->poisson_bc == HIP_POISSON_BC_NEUMANN;
+    // two iterations per sweep on one device (rb2.hpp): CFD_HIP_RB2 = 1 (the
+    // default: certified fast arithmetic), 2 (the reference's arithmetic
+    // throughout), 0 (one iteration per sweep, k_rb1)
+    const int rb2_env = getenv("CFD_HIP_RB2") ? atoi(getenv("CFD_HIP_RB2")) : 1;
+    if (neu_fold && !D && check_interval == 1 && rb2_env != 0 && c->r2geo.tiles_x > 0)
+        return relax_solve_rb2(c, rc, rel_tol, abs_tol, max_iter, rb2_env != 2);
     const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
     ST_TRY(halo(c, {c->pn}));
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
@@ -548,56 +783,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                                       it));
             }
         } else if (single) {
-            // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the
-            // end-of-step loads (experiments)
-            static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
-                                         atoi(getenv("CFD_HIP_RB1_PF")) == 0);
-            // memory hints of k_rb1 / k_rb1m (SW_* bits): FLR = 13, NT stores
-            // of Y and plain rhs loads (r03: the NT rhs loads of 15 made the
-            // neighbouring tiles re-fetch the rhs halo rows; 512^3 0.744 ->
-            // 0.726 ms, 1024^2 x 512 2.925 -> 2.85 ms, fetch 19.6 -> 18.7
-            // B/cell, profiles/r03_rbfl.jsonl)
-            // odd iterations march z downwards (REV), so each sweep starts on
-            // the planes the previous one wrote last, in the Infinity Cache;
-            // bitwise either way (kernels.hpp rb1_body). CFD_HIP_RB1_ALT=0:
-            // every iteration upwards
-            static const bool rb1_alt = !(getenv("CFD_HIP_RB1_ALT") &&
-                                          atoi(getenv("CFD_HIP_RB1_ALT")) == 0);
-            const bool rev = rb1_alt && rb1_pf && (it & 1);
-#define RB1_LAUNCH(TCV, PFV)                                                                   \
-    hipExtLaunchKernelGGL((k_rb1<FLR, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
-                          c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, c->rxst, c->partials,       \
-                          c->counter, it, (const double*)nullptr, 0, 0, (Mbox*)nullptr,        \
-                          (unsigned long long*)nullptr, neu_fold ? 1 : 0)
-            if (c->rb_strip_tc && rb1_pf) {
-                // full-width tiles and the narrow strip in one grid
-                const SGeo& gm = c->rg_main;
-                const SGeo& gs = c->rg_strip;
-                const int nbm = gm.tiles_x * gm.tiles_y * gm.tiles_z;
-                const unsigned nbt = (unsigned)(nbm + gs.tiles_x * gs.tiles_y * gs.tiles_z);
-                timed(c, HIP_KT_RELAX, [&] {
-                    auto go = [&](auto kern) {
-                        hipExtLaunchKernelGGL(kern, dim3(nbt), dim3(1024), 0, c->stream, c->ta,
-                                              c->tb, 0, gm, gs, nbm, rc, xi, xo, c->rhs, c->rxst,
-                                              c->partials, c->counter, it, neu_fold ? 1 : 0);
-                    };
-                    if (rev) go(k_rb1m<FLR, 16, true>);
-                    else go(k_rb1m<FLR, 16>);
-                }, it);
-            } else
-            timed(c, HIP_KT_RELAX, [&] {
-                if (!rb1_pf) RB1_LAUNCH(64, false);
-                else if (c->rb1_tc == 32) RB1_LAUNCH(32, true);
-                else if (c->rb1_tc == 16) RB1_LAUNCH(16, true);
-                else if (rev)
-                    hipExtLaunchKernelGGL((k_rb1<FLR, 64, true, false, true>), dim3(nb1),
-                                          dim3(1024), 0, c->stream, c->ta, c->tb, 0, c->rgeo, rc,
-                                          xi, xo, c->rhs, c->rxst, c->partials, c->counter, it,
-                                          (const double*)nullptr, 0, 0, (Mbox*)nullptr,
-                                          (unsigned long long*)nullptr, neu_fold ? 1 : 0);
-                else RB1_LAUNCH(64, true);
-            });
-#undef RB1_LAUNCH
+            rb1_sweep_single(c, rc, xi, xo, it, c->rxst, neu_fold);
         } else if (method == HIP_POISSON_REDBLACK) {
             sweep(RX_RED, xi, xo, it);
             ST_TRY(finish(it));
@@ -856,6 +1042,7 @@ static void free_ctx(hip_proj_ctx* c) {
     for (void* b : c->allocs) hipFree(b);
     if (c->st) hipFree(c->st);
     if (c->rxst) hipFree(c->rxst);
+    if (c->rxst2) hipFree(c->rxst2);
     if (c->partials) hipFree(c->partials);
     if (c->counter) hipFree(c->counter);
     if (c->red) hipFree(c->red);
@@ -993,6 +1180,25 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         rg.kc = std::max(1, std::min(rg.kc, nint_k));
         rg.tiles_z = (nint_k + rg.kc - 1) / rg.kc;
         n_partials = std::max(n_partials, rg.tiles_x * rg.tiles_y * rg.tiles_z);
+        // two RB-SOR iterations per sweep (k_rb2, rb2.hpp): 64 x 32 cells
+        // loaded, 56 x 24 written; one device, 3-D. Four partials per
+        // workgroup (two maxima, the value range).
+        SGeo& r2 = c->r2geo;
+        r2 = rg;
+        r2.tiles_x = r2.tiles_y = r2.tiles_z = 0;
+        if (c->nranks == 1 && nz > 1 && nx >= 8 && ny >= 8) {
+            r2.xofs = 0;
+            r2.tiles_x = (int)((nx - 1 + RB2_OX - 1) / RB2_OX);
+            r2.tiles_y = (int)((ny - 1 + RB2_OY - 1) / RB2_OY);
+            r2.kc = 64;
+            if (const char* e = getenv("CFD_HIP_RB2_KC")) r2.kc = std::max(1, atoi(e));
+            while (r2.kc > 4 &&
+                   (long long)r2.tiles_x * r2.tiles_y * ((nint_k + r2.kc - 1) / r2.kc) < 512)
+                r2.kc /= 2;
+            r2.kc = std::max(1, std::min(r2.kc, nint_k));
+            r2.tiles_z = (nint_k + r2.kc - 1) / r2.kc;
+            n_partials = std::max(n_partials, 2 * r2.tiles_x * r2.tiles_y * r2.tiles_z);
+        }
         // the last x tile of a TC-64 launch is partial unless 124 divides the
         // row: its workgroups run a full tile's steps for a few columns
         // (512^3: 14 of 124). Up to 28 such columns run instead as a strip

@@ -1,0 +1,583 @@
+// rb2.hpp -- two Red-Black SOR iterations per z-march (k_rb2): one device,
+// 3-D, Neumann BC folded into the stores (linear_solver_redblack.c:80-147
+// twice, with the BC of :139 between and after the iterations), driven by the
+// common loop's L-inf test (linear_solver.c:397-485) on both iterates.
+//
+// Why: one RB-SOR iteration per sweep (k_rb1) moves 24 B/cell and runs at
+// about the HBM rate its traffic allows; two iterations per sweep read X and
+// rhs and write the iterate once per two iterations (12 B/cell/iteration).
+//
+// Pipeline. Step q of the march forms, for the tile's columns,
+//   S1  R1_{q+1}: the first colour ("red", (i+j+k) odd) of X updated
+//   S2  Y1_q    : the second colour from R1          (iteration s+1 done)
+//   S3  R2_{q-1}: the first colour of Y1' (Y1 after its Neumann BC)
+//   S4  Y2_{q-2}: the second colour from R2          (iteration s+2 done)
+// with the L-inf residual of X (at plane q+1, beside S1) and of Y1' (at
+// plane q-1, beside S3). Every in-plane operand of a stage comes from the
+// plane the previous step published in LDS, every z operand from the lane's
+// own registers, so one barrier per step suffices. In step q all four
+// updates touch the same component of the lane's x pair (the colour pattern
+// is wave-uniform, as in k_rb1), and each stage's plane is stored in LDS as
+// ONE colour: R1 and R2 keep their first-colour cells, Y1 its second-colour
+// cells; the other colour of those planes is the previous stage's.
+//
+// Tiles: 32 x pairs (64 columns) x 32 rows, 1024 threads; lane l of wave w
+// owns pair l % 32 of rows w and w + 16 (same parity). Validity shrinks by
+// one cell per stage, so 56 x 24 cells are written per 64 x 32 loaded (1.52x,
+// against k_rb1's 1.38x for ONE iteration).
+//
+// Neumann BC between the iterations: the reference sets every boundary cell
+// of Y1 to its inward neighbour, and for the cells next to a face that
+// neighbour IS the cell whose stencil is evaluated; S3, S4 and the residual
+// of Y1' therefore read the centre value in place of a face cell (x / y
+// faces per lane, z faces per plane). Edge and corner cells are no interior
+// cell's neighbours. Y2 is stored with its boundary shell folded in as k_rb1
+// does. Y1 is not stored: when the loop stops on it, the host recomputes it
+// with one k_rb1 sweep from X (which this kernel leaves intact).
+//
+// APX (the product form): the SOR divisions by dx^2 / dy^2 take divc's fast
+// path without its per-division range test, and the residuals are evaluated
+// as sx/dx^2 + sy/dy^2 + sz/dz^2 - 2c(...) - b with FMAs and the SOR's own
+// neighbour sums, a few operations instead of the reference's division form.
+// Both are certified per sweep, so every decision and every stored value is
+// the reference's bit for bit:
+//  - range: the fast quotient is the correctly rounded a/d whenever |a/d| is
+//    in [2^-900, 2^900] or a = +-0 (divc / divz, tools/divc_check.c). Every
+//    value the sweep reads or writes is checked: its binary exponent >= -800
+//    (or zero) and |v| <= 2^800, which bounds every nonzero neighbour sum to
+//    [2^-852, 2^801] and the quotients into that interval for 1 <= 1/d <=
+//    2^40. A sweep that fails the check stops the loop (ST_RB2_UNCERT) and
+//    the host reruns its iterations with k_rb1.
+//  - residuals: both the reference's value and the approximation are within
+//    8u (4 M K + B) of the exact residual (u = 2^-53, M = max |v| over the
+//    sweep's values, K = 1/dx^2 + 1/dy^2 + 1/dz^2, B = max |rhs|); the loop
+//    decides only when the approximate maximum is more than E = 32u (4 M K +
+//    B) from the threshold, and otherwise stops (ST_RB2_AMBIG) for the host
+//    to compute that iterate's exact residual and resume with it. The final
+//    iterate's reported residual is always recomputed exactly by the host.
+// APX = false evaluates everything in the reference's form (divc with its
+// range test, res1) and decides exactly: the bitwise baseline of the APX form.
+#pragma once
+
+#include "kernels.hpp"
+
+namespace cfdhip {
+
+constexpr int RB2_TC = 32;   // x pairs per tile row
+constexpr int RB2_TR = 32;   // tile rows (two per wave)
+constexpr int RB2_OX = 56;   // columns written per tile
+constexpr int RB2_OY = 24;   // rows written per tile
+constexpr int ST_RB2_AMBIG = 10;   // a decision within the approximation bound (host resolves)
+constexpr int ST_RB2_UNCERT = 11;  // a value outside the certified range (host reruns exactly)
+
+struct Rb2Coef {
+    RelaxCoef rc;
+    double k2;   // 2 (RN(1/dx2) + RN(1/dy2) + inv_dz2): the centre weight of the approximation
+    double kb;   // 1/dx2 + 1/dy2 + inv_dz2 (error bound)
+    // test knobs (CFD_HIP_RB2_TEST): escale multiplies the residual bound
+    // (1e300: every decision ambiguous), elim is the least certified
+    // exponent (-800; 4096: every sweep uncertified)
+    double escale, elim;
+};
+
+// LDS of one k_rb2 workgroup (128 KB): X by plane parity, and the one-colour
+// planes of R1, Y1, R2 by plane mod 4 -- the in-plane operands of every
+// stage and the lane's own z ring (kept here rather than in registers: the
+// 16-wave workgroup caps a wave at 128 VGPRs)
+struct Rb2Lds {
+    double xs[2][RB2_TR][2][RB2_TC];  // X planes: a row's .x cells, then its .y cells
+    double r1[4][RB2_TR][RB2_TC];     // R1 first-colour cells
+    double y1[4][RB2_TR][RB2_TC];     // Y1 second-colour cells
+    double r2[4][RB2_TR][RB2_TC];     // R2 first-colour cells
+    double sh[4][16];
+    int flag;
+};
+
+// a / d for the constant divisors, fast path only (APX: certified per sweep)
+// or divc with its range test
+template <bool APX>
+__device__ __forceinline__ double rb2_div(double a, double d, double r) {
+    if constexpr (APX) {
+        const double q = a * r;
+        return fma(-fma(q, d, -a), r, q);  // divz's form: keeps the sign of a zero a
+    } else {
+        return divc(a, d, r);
+    }
+}
+
+// One SOR update from the neighbour sums sx = right + left, sy = up + down,
+// sz = above + below (linear_solver_redblack.c:103-112 order, as sor1)
+template <bool APX>
+__device__ __forceinline__ double rb2_sor(const RelaxCoef& rc, double vc, double sx, double sy,
+                                          double sz, double vb) {
+    const double pn = -(vb - rb2_div<APX>(sx, rc.dx2, rc.rdx2) -
+                        rb2_div<APX>(sy, rc.dy2, rc.rdy2) - sz * rc.inv_dz2) *
+                      rc.inv_factor;
+    return vc + rc.omega * (pn - vc);
+}
+
+// approximate |lap(x) - rhs| from the neighbour sums (see the header)
+__device__ __forceinline__ double rb2_res_apx(const Rb2Coef& cf, double c, double sx, double sy,
+                                              double sz, double b) {
+    return fabs(fma(sx, cf.rc.rdx2, fma(sy, cf.rc.rdy2, fma(sz, cf.rc.inv_dz2,
+                                                            fma(c, -cf.k2, -b)))));
+}
+
+// the binary exponent of v as frexp gives it (0 for zero)
+__device__ __forceinline__ int rb2_exp(double v) { return __builtin_amdgcn_frexp_exp(v); }
+
+// The decision of the common loop for iterate `it` >= 1 (check_interval 1)
+// from an approximate residual maximum m with bound E; false = ambiguous.
+__device__ __forceinline__ bool rb2_decide(RxState* st, double m, double E, int it) {
+    const double thr = fmax(st->tol, st->abs_tol);  // m < tol || m < abs_tol
+    bool conv;
+    if (st->ovr_it == it) {
+        m = st->ovr_m;
+        conv = m < thr;
+        st->res_exact = 1;
+    } else if (m + E < thr) {
+        conv = true;
+        st->res_exact = 0;
+    } else if (m - E >= thr) {
+        conv = false;
+        st->res_exact = 0;
+    } else {
+        st->done = 1;
+        st->status = ST_RB2_AMBIG;
+        st->res_it = it;
+        return false;
+    }
+    st->res = m;
+    if (conv) {
+        st->done = 1;
+        st->status = ST_CONVERGED;
+        st->iterations = it;
+        st->res_it = it;
+    } else if (it >= st->max_iter) {
+        st->done = 1;
+        st->status = ST_MAX_ITER;
+        st->iterations = st->max_iter + 1;
+        st->res_it = it;
+    }
+    return true;
+}
+
+// X = iterate s (s >= 1, its boundary shell Neumann), Y <- iterate s + 2.
+// certx: certify X's values too (the first sweep after a k_rb1 sweep).
+// The march of one k_rb2 tile (see the header); BND: the tile touches the
+// faces (per-lane face, range and shell logic), else all of it folds away.
+template <bool APX, int FL, bool BND>
+__device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coef& cf,
+                                          const double* __restrict__ X, double* __restrict__ Y,
+                                          const double* __restrict__ rhs, int c, int r, int i0,
+                                          int j, int kb, int ke, int certx, double& mX,
+                                          double& mY, double& M, int& emin) {
+    const RelaxCoef& rc = cf.rc;
+    const int cm = max(c - 1, 0), cp = min(c + 1, RB2_TC - 1);
+    const int rlo = max(r - 1, 0), rhi = min(r + 1, RB2_TR - 1);
+    // BND = false: the tile's loaded cells are all interior and none is next
+    // to an x / y face, so every per-lane face and range test folds away
+    const bool jin = !BND || (j >= 1 && j <= g.ny - 2);
+    const bool in0 = !BND || (jin && i0 >= 1 && i0 <= g.nx - 2);
+    const bool in1 = !BND || (jin && i0 + 1 <= g.nx - 2);
+    const bool own = (c >= 2 && c <= RB2_TC - 3) && (r >= 4 && r <= RB2_TR - 5);
+    const bool own0 = own && in0, own1 = own && in1;
+    // the folded Neumann shell of Y2 (as k_rb1's nrole): 1 = pair (0, 1),
+    // 2 = pair (nx-2, nx-1), 4 = nx odd and .y is cell nx-2, 8 = store
+    const int nrole = BND ? ((i0 == 0 ? 1 : 0) | (i0 + 1 == g.nx - 1 ? 2 : 0) |
+                             (i0 + 1 == g.nx - 2 ? 4 : 0) |
+                             ((own && jin && i0 <= g.nx - 2) ? 8 : 0))
+                          : (own ? 8 : 0);
+    // face neighbours of iteration 2 (read as the centre): per component,
+    // the x- / x+ neighbour is a face cell; y- / y+ per row
+    const bool f0r = BND && (i0 + 1 == g.nx - 1);  // .x's right neighbour (own .y)
+    const bool f1l = BND && (i0 == 0);              // .y's left neighbour (own .x)
+    const bool f1r = BND && (i0 + 2 == g.nx - 1);   // .y's right neighbour (pair c+1 .x)
+    const bool fdn = BND && (j == 1), fup = BND && (j == g.ny - 2);
+    // loads from clamped, always valid addresses (see k_rb1): values outside
+    // the grid only feed boundary cells and halo lanes
+    const int ic = (i0 < g.nx) ? max(i0, 0) : g.nx - 2 - ((g.nx - 2) & 1);
+    const long long colx = (long long)max(min(j, g.ny - 1), 0) * g.px + ic;
+    const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
+    auto ldx = [&](int k) -> double2 {
+        return ld2(X, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx);
+    };
+    auto ldr = [&](int k) -> double2 {
+        return ld2(rhs, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx);
+    };
+    auto comp = [](const double2& v, int e) __attribute__((always_inline)) {
+        return e == 0 ? v.x : v.y;
+    };
+    const int q0 = kb - 4;
+    double2 xr[4], br[4];
+    xr[0] = ldx(q0);
+    xr[1] = ldx(q0 + 1);
+    xr[2] = ldx(q0 + 2);
+    xr[3] = make_double2(0.0, 0.0);
+    br[0] = br[1] = br[3] = make_double2(0.0, 0.0);
+    br[2] = ldr(q0 + 1);
+    // X_{q0+1} into the X slot step q0 reads: LDS slots count planes from q0
+    L.xs[1][r][0][c] = xr[1].x;
+    L.xs[1][r][1][c] = xr[1].y;
+    auto cert = [&](bool ok, double v) __attribute__((always_inline)) {
+        if constexpr (APX) {
+            if (ok) {
+                M = fmax(M, fabs(v));
+                emin = min(emin, rb2_exp(v));
+            }
+        }
+    };
+    const int nzi = g.nz - 2;  // last interior plane
+    auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
+        constexpr bool E = decltype(Ec)::value;
+        constexpr int P = decltype(Pc)::value;
+        constexpr int e = E ? 0 : 1;  // the component every update of this step touches
+        // register rings (X, rhs): slot of plane p = (P + p - q + off) & 3
+        constexpr int X0 = P & 3, X1 = (P + 1) & 3, X2 = (P + 2) & 3, X3 = (P + 3) & 3;
+        constexpr int Bm1 = P & 3, B0 = (P + 1) & 3, B1 = (P + 2) & 3, B2 = (P + 3) & 3;
+        // LDS slots of plane p: (P + p - q) & 1 (X) or & 3 (R1, Y1, R2)
+        constexpr int LX1 = (P + 1) & 1, LX2 = P & 1;  // X_{q+1} read, X_{q+2} written
+        constexpr int A1n = (P + 1) & 3, A1c = P & 3, A1m = (P + 3) & 3, A1mm = (P + 2) & 3;
+        constexpr int AYn = P & 3, AYm = (P + 3) & 3, AYmm = (P + 2) & 3;
+        constexpr int A2n = (P + 3) & 3, A2m = (P + 2) & 3, A2mm = (P + 1) & 3;
+        // rhs_{q-2} leaves its slot to rhs_{q+2}
+        const double bq2 = comp(br[B2], e);
+        xr[X3] = ldx(q + 3);
+        br[B2] = ldr(q + 2);
+        __syncthreads();
+        const double2 Xm = xr[X0], Xc = xr[X1], Xp = xr[X2];
+        // ---- S1: R1_{q+1} (+ L-inf residual of X at plane q+1) ----
+        const int qa = q + 1;
+        const bool pin1 = (qa >= 1 && qa <= nzi);
+        const double2 xlo = make_double2(L.xs[LX1][rlo][0][c], L.xs[LX1][rlo][1][c]);
+        const double2 xhi = make_double2(L.xs[LX1][rhi][0][c], L.xs[LX1][rhi][1][c]);
+        const double xlp = L.xs[LX1][r][1][cm];  // pair c-1 .y
+        const double xrp = L.xs[LX1][r][0][cp];  // pair c+1 .x
+        const double2 b1 = br[B1];
+        // neighbour sums (right + left, up + down, above + below) of both cells
+        const double sx0 = Xc.y + xlp, sy0 = xhi.x + xlo.x, sz0 = Xp.x + Xm.x;
+        const double sx1 = xrp + Xc.x, sy1 = xhi.y + xlo.y, sz1 = Xp.y + Xm.y;
+        double r1v;
+        if (e == 0) {
+            const double v = rb2_sor<APX>(rc, Xc.x, sx0, sy0, sz0, b1.x);
+            r1v = (pin1 && in0) ? v : Xc.x;
+        } else {
+            const double v = rb2_sor<APX>(rc, Xc.y, sx1, sy1, sz1, b1.y);
+            r1v = (pin1 && in1) ? v : Xc.y;
+        }
+        if (qa >= kb && qa < ke) {
+            double a0, a1;
+            if constexpr (APX) {
+                a0 = rb2_res_apx(cf, Xc.x, sx0, sy0, sz0, b1.x);
+                a1 = rb2_res_apx(cf, Xc.y, sx1, sy1, sz1, b1.y);
+            } else {
+                a0 = res1(rc, DivC{}, Xc.x, xlp, Xc.y, xlo.x, xhi.x, Xm.x, Xp.x, b1.x);
+                a1 = res1(rc, DivC{}, Xc.y, Xc.x, xrp, xlo.y, xhi.y, Xm.y, Xp.y, b1.y);
+            }
+            if (own0 && a0 > mX) mX = a0;
+            if (own1 && a1 > mX) mX = a1;
+            if (certx) {
+                cert(own0, Xc.x);
+                cert(own1, Xc.y);
+            }
+            cert(e == 0 ? own0 : own1, r1v);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the stages' live ranges apart
+        // ---- S2: Y1_q, second colour (component e) from R1 ----
+        const bool pin0 = (q >= 1 && q <= nzi);
+        const double r1c = L.r1[A1c][r][c];  // the pair's first-colour cell of R1_q
+        const double r1m = L.r1[A1m][r][c];  // ... of R1_{q-1} (= Y1' there)
+        double y1v;
+        {
+            const double rdn = L.r1[A1c][rlo][c], rup = L.r1[A1c][rhi][c];
+            const double rsd = (e == 0) ? L.r1[A1c][r][cm] : L.r1[A1c][r][cp];
+            const double sx = (e == 0) ? r1c + rsd : rsd + r1c;
+            const double v = rb2_sor<APX>(rc, comp(Xm, e), sx, rup + rdn, r1v + r1m,
+                                          comp(br[B0], e));
+            y1v = (pin0 && (e == 0 ? in0 : in1)) ? v : comp(Xm, e);
+            if (q >= kb && q < ke) cert(e == 0 ? own0 : own1, y1v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- S3: R2_{q-1} from Y1' (+ L-inf residual of Y1' at plane q-1) ----
+        const int qc = q - 1;
+        const bool pinm = (qc >= 1 && qc <= nzi);
+        const double y1mm = L.y1[AYmm][r][c];  // Y1' second-colour cell at q-2 (= R2 there)
+        double r2v;
+        {
+            const double cen = r1m;                 // Y1' first-colour cell at q-1
+            const double ob = L.y1[AYm][r][c];      // the pair's second-colour cell at q-1
+            double ydn = L.y1[AYm][rlo][c], yup = L.y1[AYm][rhi][c];
+            const double ysd = (e == 0) ? L.y1[AYm][r][cm] : L.y1[AYm][r][cp];
+            double zm = y1mm, zp = y1v;
+            if (qc == 1) zm = cen;
+            if (qc == nzi) zp = cen;
+            if (fdn) ydn = cen;
+            if (fup) yup = cen;
+            double lf, rt;
+            if (e == 0) {
+                lf = ysd;
+                rt = f0r ? cen : ob;
+            } else {
+                lf = f1l ? cen : ob;
+                rt = f1r ? cen : ysd;
+            }
+            const double sx = rt + lf, sy = yup + ydn, sz = zp + zm;
+            const double2 bm = br[Bm1];
+            const double v = rb2_sor<APX>(rc, cen, sx, sy, sz, comp(bm, e));
+            r2v = (pinm && (e == 0 ? in0 : in1)) ? v : cen;
+            if (qc >= kb && qc < ke) {
+                // the residual of Y1' at plane q-1: cell e (first colour)
+                // shares the update's sums; cell 1-e (second colour, value ob)
+                // reads the first-colour cells of Y1' = R1 at q-1
+                const double cb = ob;
+                double rdn = L.r1[A1m][rlo][c], rup = L.r1[A1m][rhi][c];
+                const double rsd = (e == 0) ? L.r1[A1m][r][cp] : L.r1[A1m][r][cm];
+                double wm = L.r1[A1mm][r][c], wp = r1c;
+                if (qc == 1) wm = cb;
+                if (qc == nzi) wp = cb;
+                if (fdn) rdn = cb;
+                if (fup) rup = cb;
+                double lf2, rt2;
+                if (e == 0) {  // cell 1 (.y): left own .x (first colour), right pair c+1 .x
+                    lf2 = f1l ? cb : cen;
+                    rt2 = f1r ? cb : rsd;
+                } else {       // cell 0 (.x): left pair c-1 .y, right own .y
+                    lf2 = rsd;
+                    rt2 = f0r ? cb : cen;
+                }
+                double ae, ab;
+                if constexpr (APX) {
+                    ae = rb2_res_apx(cf, cen, sx, sy, sz, comp(bm, e));
+                    ab = rb2_res_apx(cf, cb, rt2 + lf2, rup + rdn, wp + wm, comp(bm, 1 - e));
+                } else {
+                    ae = res1(rc, DivC{}, cen, lf, rt, ydn, yup, zm, zp, comp(bm, e));
+                    ab = res1(rc, DivC{}, cb, lf2, rt2, rdn, rup, wm, wp, comp(bm, 1 - e));
+                }
+                const bool oe = (e == 0) ? own0 : own1, ob_ = (e == 0) ? own1 : own0;
+                if (oe && ae > mY) mY = ae;
+                if (ob_ && ab > mY) mY = ab;
+                cert(oe, r2v);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- S4: Y2_{q-2}, second colour from R2 -> stored ----
+        const int qd = q - 2;
+        {
+            const bool pind = (qd >= 1 && qd <= nzi);
+            const double cen = y1mm;             // Y1' second-colour cell at q-2
+            const double ow = L.r2[A2m][r][c];   // the pair's first-colour cell of R2 at q-2
+            double wdn = L.r2[A2m][rlo][c], wup = L.r2[A2m][rhi][c];
+            const double wsd = (e == 0) ? L.r2[A2m][r][cm] : L.r2[A2m][r][cp];
+            double zm = L.r2[A2mm][r][c], zp = r2v;
+            if (qd == 1) zm = cen;
+            if (qd == nzi) zp = cen;
+            if (fdn) wdn = cen;
+            if (fup) wup = cen;
+            double lf, rt;
+            if (e == 0) {
+                lf = wsd;
+                rt = f0r ? cen : ow;
+            } else {
+                lf = f1l ? cen : ow;
+                rt = f1r ? cen : wsd;
+            }
+            const double v = rb2_sor<APX>(rc, cen, rt + lf, wup + wdn, zp + zm, bq2);
+            const double y2v = (pind && (e == 0 ? in0 : in1)) ? v : cen;
+            if (qd >= kb && qd < ke) {
+                cert(e == 0 ? own0 : own1, y2v);
+                double2 out = (e == 0) ? make_double2(y2v, ow) : make_double2(ow, y2v);
+                // the Neumann shell folded into the stores (as k_rb1)
+                if (nrole & 1) out.x = out.y;
+                if (nrole & 2) out.y = out.x;
+                if (nrole & 8) {
+                    auto put = [&](long long base) __attribute__((always_inline)) {
+                        st2v<FL>(Y, base, out);
+                        if (nrole & 4) Y[base + 2] = out.y;
+                        if (BND && (j == 1 || j == g.ny - 2)) {
+                            const long long b2 = base + (j == 1 ? -g.px : g.px);
+                            st2v<FL>(Y, b2, out);
+                            if (nrole & 4) Y[b2 + 2] = out.y;
+                        }
+                    };
+                    const long long base = (long long)qd * g.ps + col;
+                    put(base);
+                    if (qd == 1) put(base - g.ps);
+                    if (qd == nzi) put(base + g.ps);
+                }
+            }
+        }
+        // ---- publish for step q + 1 ----
+        L.xs[LX2][r][0][c] = Xp.x;
+        L.xs[LX2][r][1][c] = Xp.y;
+        L.r1[A1n][r][c] = r1v;
+        L.y1[AYn][r][c] = y1v;
+        L.r2[A2n][r][c] = r2v;
+    };
+    // E(q) = ((j + q + kofs) & 1) == 0, wave-uniform (rows r and r + 16 share it)
+    const bool E0 = __builtin_amdgcn_readfirstlane(((j + q0 + g.kofs) & 1) == 0 ? 1 : 0) != 0;
+    const int nsteps = ke - kb + 6;  // q0 .. ke + 1
+    int n = 0;
+    auto march = [&](auto E0c) __attribute__((always_inline)) {
+        constexpr bool A = decltype(E0c)::value;
+        using TA = BoolC<A>;
+        using TB = BoolC<!A>;
+        for (; n + 3 < nsteps; n += 4) {
+            step(TA{}, IntC<0>{}, q0 + n);
+            step(TB{}, IntC<1>{}, q0 + n + 1);
+            step(TA{}, IntC<2>{}, q0 + n + 2);
+            step(TB{}, IntC<3>{}, q0 + n + 3);
+        }
+        if (n < nsteps) step(TA{}, IntC<0>{}, q0 + n);
+        if (n + 1 < nsteps) step(TB{}, IntC<1>{}, q0 + n + 1);
+        if (n + 2 < nsteps) step(TA{}, IntC<2>{}, q0 + n + 2);
+    };
+    if (E0) march(BoolC<true>{});
+    else march(BoolC<false>{});
+}
+
+template <bool APX, int FL>
+static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
+                                                       const double* __restrict__ X,
+                                                       double* __restrict__ Y,
+                                                       const double* __restrict__ rhs,
+                                                       RxState* st, double* partials,
+                                                       unsigned* counter, int s, int certx) {
+    __shared__ Rb2Lds L;
+    if (st->done) return;
+    const int t = blockIdx.x;
+    const int tx = t % g.tiles_x;
+    const int rest = t / g.tiles_x;
+    const int ty = rest % g.tiles_y;
+    const int tz = rest / g.tiles_y;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int c = lane & 31;
+    const int r = w + 16 * (lane >> 5);
+    const int i0 = tx * RB2_OX - 4 + 2 * c;  // even; the pair is (i0, i0 + 1)
+    const int j = ty * RB2_OY - 4 + r;
+    const int kb = g.k0 + tz * g.kc;
+    const int ke = min(kb + g.kc, g.k1);
+    // does the tile touch the faces (its loaded cells reach i < 1,
+    // i > nx - 3, j < 2 or j > ny - 3)?
+    const int ilo = tx * RB2_OX - 4, jlo = ty * RB2_OY - 4;
+    const bool bnd = !(ilo >= 1 && ilo + 2 * RB2_TC - 1 <= g.nx - 3 && jlo >= 2 &&
+                       jlo + RB2_TR - 1 <= g.ny - 3);
+    double mX = 0.0, mY = 0.0, M = 0.0;
+    int emin = 0;
+    if (bnd)
+        rb2_march<APX, FL, true>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M, emin);
+    else
+        rb2_march<APX, FL, false>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M,
+                                  emin);
+    // ---- the sweep's maxima: partials[4 b + 0..3]; the last workgroup decides ----
+    mX = wave_max(mX);
+    mY = wave_max(mY);
+    if constexpr (APX) {
+        M = wave_max(M);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) emin = min(emin, __shfl_down(emin, off, 64));
+    }
+    if (lane == 0) {
+        L.sh[0][w] = mX;
+        L.sh[1][w] = mY;
+        L.sh[2][w] = M;
+        L.sh[3][w] = (double)emin;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0, mm = 0.0, em = 0.0;
+        for (int v = 0; v < 16; ++v) {
+            a = fmax(a, L.sh[0][v]);
+            b = fmax(b, L.sh[1][v]);
+            mm = fmax(mm, L.sh[2][v]);
+            em = fmin(em, L.sh[3][v]);
+        }
+        store_sc1(&partials[4 * blockIdx.x + 0], a);
+        store_sc1(&partials[4 * blockIdx.x + 1], b);
+        store_sc1(&partials[4 * blockIdx.x + 2], mm);
+        store_sc1(&partials[4 * blockIdx.x + 3], em);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned tk = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        L.flag = (tk == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (L.flag == 0) return;
+    double a = 0.0, b = 0.0, mm = 0.0, em = 0.0;
+    for (unsigned blk = threadIdx.x; blk < gridDim.x; blk += 1024) {
+        a = fmax(a, load_sc1(&partials[4 * blk + 0]));
+        b = fmax(b, load_sc1(&partials[4 * blk + 1]));
+        mm = fmax(mm, load_sc1(&partials[4 * blk + 2]));
+        em = fmin(em, load_sc1(&partials[4 * blk + 3]));
+    }
+    a = wave_max(a);
+    b = wave_max(b);
+    mm = wave_max(mm);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) em = fmin(em, __shfl_down(em, off, 64));
+    __syncthreads();
+    if (lane == 0) {
+        L.sh[0][w] = a;
+        L.sh[1][w] = b;
+        L.sh[2][w] = mm;
+        L.sh[3][w] = em;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tX = 0.0, tY = 0.0, tM = 0.0, tE = 0.0;
+        for (int v = 0; v < 16; ++v) {
+            tX = fmax(tX, L.sh[0][v]);
+            tY = fmax(tY, L.sh[1][v]);
+            tM = fmax(tM, L.sh[2][v]);
+            tE = fmin(tE, L.sh[3][v]);
+        }
+        __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (APX) {
+            if (tE < cf.elim || !(tM <= 0x1p800)) {
+                st->done = 1;
+                st->status = ST_RB2_UNCERT;
+                st->res_it = s;
+                return;
+            }
+            const double E = 32.0 * 0x1p-53 * (4.0 * tM * cf.kb + st->bmax) * cf.escale;
+            if (rb2_decide(st, tX, E, s) && !st->done) rb2_decide(st, tY, E, s + 1);
+        } else {
+            rx_finish(st, tX, s);
+            if (!st->done) rx_finish(st, tY, s + 1);
+        }
+    }
+}
+
+// max |rhs| over the interior (the residual bound's B), into st->bmax; one
+// workgroup per block of planes, atomic max on the bit pattern (|v| >= 0
+// orders as its bits)
+static __global__ __launch_bounds__(256) void k_rb2_bmax(Geo g, const double* __restrict__ rhs,
+                                                         RxState* st) {
+    double m = 0.0;
+    const long long plane = (long long)g.nx * g.ny;
+    const long long total = plane * g.nz;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int k = (int)(e / plane);
+        const long long q = e % plane;
+        const int jj = (int)(q / g.nx), ii = (int)(q % g.nx);
+        m = fmax(m, fabs(rhs[(long long)k * g.ps + (long long)jj * g.px + ii]));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0 && m > 0.0)
+        __hip_atomic_fetch_max((gu64*)&st->bmax, (unsigned long long)__double_as_longlong(m),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// resume the loop after the host resolved a stop: clear the decision, and
+// with ovr_it >= 0 give the loop that iterate's exact residual
+static __global__ void k_rb2_resume(RxState* st, int ovr_it, double ovr_m) {
+    if (threadIdx.x == 0) {
+        st->done = 0;
+        st->status = ST_MAX_ITER;
+        st->ovr_it = ovr_it;
+        st->ovr_m = ovr_m;
+    }
+}
+
+}  // namespace cfdhip

@@ -1,0 +1,11 @@
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+for m in 0 1 2; do
+  for g in "512 512 512" "1024 1024 512"; do
+    set -- $g
+    CFD_HIP_RB2=$m NX=$1 NY=$2 NZ=$3 ITERS=200 METHODS=rbsor timeout -k 10 120 python tools/relax_bench.py >> gpurun_out/r04_rb2_perf.jsonl 2>>gpurun_out/r04_rb2_perf.err || exit 1
+    echo "rb2=$m $g done"
+  done
+done
+timeout -k 10 300 python bench.py --case convection --steps 1 --warmup 0 > gpurun_out/r04_conv_rb2.json 2> gpurun_out/r04_conv_rb2.err || exit 1
+echo conv done
