@@ -526,6 +526,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     double* by = c->xt;
     int cur = 0;
     bool exact_mode = false, force_certx = false;
+    int n_ambig = 0, n_uncert = 0;
     auto launch = [&]() {
         if (cur == 0 || exact_mode) {
             rb1_sweep_single(c, rc, bx, by, cur, c->rxst, true);
@@ -534,7 +535,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         } else {
             const int certx = (force_certx || log.empty() || log.back().kind == 1) ? 1 : 0;
             force_certx = false;
-            timed(c, HIP_KT_RELAX, [&] {
+            timed(c, HIP_KT_RELAX2, [&] {
                 if (apx)
                     hipExtLaunchKernelGGL((k_rb2<true, FLR>), dim3(nb2), dim3(1024), 0, c->stream,
                                           c->ta, c->tb, 0, g2, cf, (const double*)bx, by,
@@ -606,6 +607,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         }
         const Launch L = log[li];
         if (r.status == ST_RB2_UNCERT) {
+            ++n_uncert;
             // rerun from this sweep's input with k_rb1 sweeps
             log.resize(li);
             exact_mode = true;
@@ -619,6 +621,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         double* xt = mid ? L.y : L.x;
         if (mid) recompute_mid(L);
         if (r.status == ST_RB2_AMBIG) {
+            ++n_ambig;
             double m = 0.0;
             ST_TRY(residual_linf(c, xt, resc, &m));
             log.resize(li);
@@ -633,6 +636,13 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         flush_timing(c);
         double res = r.res;
         if (!r.res_exact) ST_TRY(residual_linf(c, xt, resc, &res));
+        if (getenv("CFD_HIP_RB2_LOG")) {  // diagnostics: the loop's launches and stops
+            int n1 = 0, n2 = 0;
+            for (const Launch& q : log) (q.kind == 1 ? n1 : n2)++;
+            fprintf(stderr, "rb2: iterations %d status %d, k_rb1 %d k_rb2 %d launches, "
+                    "%d ambiguous, %d uncertified, res_it %d\n", r.iterations, r.status, n1, n2,
+                    n_ambig, n_uncert, r.res_it);
+        }
         if (xt != c->pn) std::swap(c->pn, c->xt);
         c->pstats.initial_residual = r.res0;
         c->pstats.iterations = r.iterations;

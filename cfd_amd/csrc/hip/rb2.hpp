@@ -80,15 +80,19 @@ struct Rb2Coef {
     double escale, elim;
 };
 
-// LDS of one k_rb2 workgroup (128 KB): X by plane parity, and the one-colour
+// LDS of one k_rb2 workgroup (148 KB): X by plane parity, and the one-colour
 // planes of R1, Y1, R2 by plane mod 4 -- the in-plane operands of every
 // stage and the lane's own z ring (kept here rather than in registers: the
-// 16-wave workgroup caps a wave at 128 VGPRs)
+// 16-wave workgroup caps a wave at 128 VGPRs). Every plane has a one-cell
+// pad around the tile (never written: it feeds halo lanes only), so a lane
+// reaches its four neighbours at fixed offsets from ONE address, which
+// keeps the address registers to a couple instead of one per neighbour.
+constexpr int RB2_LP = RB2_TC + 2;             // padded row (doubles)
+constexpr int RB2_LS = (RB2_TR + 2) * RB2_LP;  // padded one-colour plane
+// planes: 0-3 X (slot * 2 + component), 4-7 R1, 8-11 Y1, 12-15 R2 (by slot)
+constexpr int RB2_PX = 0, RB2_PR1 = 4, RB2_PY1 = 8, RB2_PR2 = 12;
 struct Rb2Lds {
-    double xs[2][RB2_TR][2][RB2_TC];  // X planes: a row's .x cells, then its .y cells
-    double r1[4][RB2_TR][RB2_TC];     // R1 first-colour cells
-    double y1[4][RB2_TR][RB2_TC];     // Y1 second-colour cells
-    double r2[4][RB2_TR][RB2_TC];     // R2 first-colour cells
+    double pl[16][RB2_LS];
     double sh[4][16];
     int flag;
 };
@@ -173,8 +177,20 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                                           int j, int kb, int ke, int certx, double& mX,
                                           double& mY, double& M, int& emin) {
     const RelaxCoef& rc = cf.rc;
-    const int cm = max(c - 1, 0), cp = min(c + 1, RB2_TC - 1);
-    const int rlo = max(r - 1, 0), rhi = min(r + 1, RB2_TR - 1);
+    // LDS addressing: two per-lane bases (planes 0-7 and 8-15), each at the
+    // lane's cell minus one row and one column, so every operand is a
+    // non-negative immediate offset below 64 KB (a negative or larger offset
+    // makes the compiler keep one address register per access)
+    double* const Lb0 = &L.pl[0][r * RB2_LP + c];
+    double* const Lb1 = &L.pl[8][r * RB2_LP + c];
+    constexpr int OWN = RB2_LP + 1, LF = RB2_LP, RT = RB2_LP + 2, DNo = 1, UPo = 2 * RB2_LP + 1;
+    auto ld = [&](int plane, int d) __attribute__((always_inline)) -> double {
+        return plane < 8 ? Lb0[plane * RB2_LS + d] : Lb1[(plane - 8) * RB2_LS + d];
+    };
+    auto st = [&](int plane, double v) __attribute__((always_inline)) {
+        if (plane < 8) Lb0[plane * RB2_LS + OWN] = v;
+        else Lb1[(plane - 8) * RB2_LS + OWN] = v;
+    };
     // BND = false: the tile's loaded cells are all interior and none is next
     // to an x / y face, so every per-lane face and range test folds away
     const bool jin = !BND || (j >= 1 && j <= g.ny - 2);
@@ -197,13 +213,15 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     // loads from clamped, always valid addresses (see k_rb1): values outside
     // the grid only feed boundary cells and halo lanes
     const int ic = (i0 < g.nx) ? max(i0, 0) : g.nx - 2 - ((g.nx - 2) & 1);
-    const long long colx = (long long)max(min(j, g.ny - 1), 0) * g.px + ic;
-    const long long col = (long long)max(min(j, g.ny - 1), 0) * g.px + max(i0, 0);
+    // 32-bit offsets within a plane from a wave-uniform plane base
+    const int colx = max(min(j, g.ny - 1), 0) * (int)g.px + ic;
+    const int col = max(min(j, g.ny - 1), 0) * (int)g.px + max(i0, 0);
+    const int px = (int)g.px;
     auto ldx = [&](int k) -> double2 {
-        return ld2(X, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx);
+        return ld2(X + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
     };
     auto ldr = [&](int k) -> double2 {
-        return ld2(rhs, (long long)min(max(k, 0), g.nz - 1) * g.ps + colx);
+        return ld2(rhs + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
     };
     auto comp = [](const double2& v, int e) __attribute__((always_inline)) {
         return e == 0 ? v.x : v.y;
@@ -217,15 +235,27 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     br[0] = br[1] = br[3] = make_double2(0.0, 0.0);
     br[2] = ldr(q0 + 1);
     // X_{q0+1} into the X slot step q0 reads: LDS slots count planes from q0
-    L.xs[1][r][0][c] = xr[1].x;
-    L.xs[1][r][1][c] = xr[1].y;
+    st(RB2_PX + 2, xr[1].x);
+    st(RB2_PX + 3, xr[1].y);
+    // certification of one value (APX): branch-free, so the step stays one
+    // basic block and its LDS reads can be scheduled ahead of the arithmetic
     auto cert = [&](bool ok, double v) __attribute__((always_inline)) {
         if constexpr (APX) {
-            if (ok) {
-                M = fmax(M, fabs(v));
-                emin = min(emin, rb2_exp(v));
-            }
+            const double av = fabs(v);
+            M = (ok && av > M) ? av : M;
+            const int ev = rb2_exp(v);
+            emin = (ok && ev < emin) ? ev : emin;
         }
+    };
+    auto umax = [](bool ok, double a, double m) __attribute__((always_inline)) {
+        return (ok && a > m) ? a : m;
+    };
+    // pin the running maxima at the end of their stage: left alone, the
+    // compiler sinks every residual and range update of the unrolled steps
+    // to the loop's back edge, where their operands no longer fit in VGPRs
+    auto pin = [&]() __attribute__((always_inline)) {
+        asm volatile("" : "+v"(mX), "+v"(mY));
+        if constexpr (APX) asm volatile("" : "+v"(M), "+v"(emin));
     };
     const int nzi = g.nz - 2;  // last interior plane
     auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
@@ -240,20 +270,39 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         constexpr int A1n = (P + 1) & 3, A1c = P & 3, A1m = (P + 3) & 3, A1mm = (P + 2) & 3;
         constexpr int AYn = P & 3, AYm = (P + 3) & 3, AYmm = (P + 2) & 3;
         constexpr int A2n = (P + 3) & 3, A2m = (P + 2) & 3, A2mm = (P + 1) & 3;
+        // the one-colour neighbour of the updated component e on its x side
+        // (pair c-1 for .x, pair c+1 for .y), and the other side's
+        constexpr int SD = (e == 0) ? LF : RT, SDo = (e == 0) ? RT : LF;
         // rhs_{q-2} leaves its slot to rhs_{q+2}
         const double bq2 = comp(br[B2], e);
         xr[X3] = ldx(q + 3);
         br[B2] = ldr(q + 2);
         __syncthreads();
+        const int qa = q + 1, qc = q - 1, qd = q - 2;
+        const bool pin1 = (qa >= 1 && qa <= nzi), pin0 = (q >= 1 && q <= nzi);
+        const bool pinm = (qc >= 1 && qc <= nzi), pind = (qd >= 1 && qd <= nzi);
+        const bool oka = (qa >= kb && qa < ke), ok0 = (q >= kb && q < ke);
+        const bool okc = (qc >= kb && qc < ke), okd = (qd >= kb && qd < ke);
+        const bool ine = (e == 0) ? in0 : in1;
+        const bool owe = (e == 0) ? own0 : own1, owb = (e == 0) ? own1 : own0;
+        // ---- LDS operands of S1 and S2 ----
+        constexpr int PX0 = RB2_PX + 2 * LX1, PX1 = PX0 + 1;
+        const double2 xlo = make_double2(ld(PX0, DNo), ld(PX1, DNo));
+        const double2 xhi = make_double2(ld(PX0, UPo), ld(PX1, UPo));
+        const double xlp = ld(PX1, LF);  // pair c-1 .y
+        const double xrp = ld(PX0, RT);  // pair c+1 .x
+        const double r1c = ld(RB2_PR1 + A1c, OWN);  // the pair's first-colour cell of R1_q
+        const double r1m = ld(RB2_PR1 + A1m, OWN);  // ... of R1_{q-1} (= Y1' there)
+        const double r1dn = ld(RB2_PR1 + A1c, DNo), r1up = ld(RB2_PR1 + A1c, UPo);
+        const double r1sd = ld(RB2_PR1 + A1c, SD);
         const double2 Xm = xr[X0], Xc = xr[X1], Xp = xr[X2];
-        // ---- S1: R1_{q+1} (+ L-inf residual of X at plane q+1) ----
-        const int qa = q + 1;
-        const bool pin1 = (qa >= 1 && qa <= nzi);
-        const double2 xlo = make_double2(L.xs[LX1][rlo][0][c], L.xs[LX1][rlo][1][c]);
-        const double2 xhi = make_double2(L.xs[LX1][rhi][0][c], L.xs[LX1][rhi][1][c]);
-        const double xlp = L.xs[LX1][r][1][cm];  // pair c-1 .y
-        const double xrp = L.xs[LX1][r][0][cp];  // pair c+1 .x
         const double2 b1 = br[B1];
+        // scheduling fences: each group of LDS reads is issued ahead of the
+        // stage before the one that consumes it (its latency hides behind
+        // that stage's arithmetic), and no group is hoisted further (the
+        // operands of all four stages at once do not fit in 128 VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- S1: R1_{q+1} (+ L-inf residual of X at plane q+1) ----
         // neighbour sums (right + left, up + down, above + below) of both cells
         const double sx0 = Xc.y + xlp, sy0 = xhi.x + xlo.x, sz0 = Xp.x + Xm.x;
         const double sx1 = xrp + Xc.x, sy1 = xhi.y + xlo.y, sz1 = Xp.y + Xm.y;
@@ -265,7 +314,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             const double v = rb2_sor<APX>(rc, Xc.y, sx1, sy1, sz1, b1.y);
             r1v = (pin1 && in1) ? v : Xc.y;
         }
-        if (qa >= kb && qa < ke) {
+        {
             double a0, a1;
             if constexpr (APX) {
                 a0 = rb2_res_apx(cf, Xc.x, sx0, sy0, sz0, b1.x);
@@ -274,45 +323,46 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 a0 = res1(rc, DivC{}, Xc.x, xlp, Xc.y, xlo.x, xhi.x, Xm.x, Xp.x, b1.x);
                 a1 = res1(rc, DivC{}, Xc.y, Xc.x, xrp, xlo.y, xhi.y, Xm.y, Xp.y, b1.y);
             }
-            if (own0 && a0 > mX) mX = a0;
-            if (own1 && a1 > mX) mX = a1;
-            if (certx) {
-                cert(own0, Xc.x);
-                cert(own1, Xc.y);
-            }
-            cert(e == 0 ? own0 : own1, r1v);
+            mX = umax(oka && own0, a0, mX);
+            mX = umax(oka && own1, a1, mX);
+            cert(oka && certx && own0, Xc.x);
+            cert(oka && certx && own1, Xc.y);
+            cert(oka && owe, r1v);
+            pin();
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep the stages' live ranges apart
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- LDS operands of S3, the residual of Y1' and S4 ----
+        const double y1mm = ld(RB2_PY1 + AYmm, OWN);  // Y1' second-colour cell at q-2 (= R2)
+        const double ob = ld(RB2_PY1 + AYm, OWN);     // the pair's second-colour cell at q-1
+        double ydn = ld(RB2_PY1 + AYm, DNo), yup = ld(RB2_PY1 + AYm, UPo);
+        const double ysd = ld(RB2_PY1 + AYm, SD);
+        double qdn = ld(RB2_PR1 + A1m, DNo), qup = ld(RB2_PR1 + A1m, UPo);
+        const double qsd = ld(RB2_PR1 + A1m, SDo);
+        double wm1 = ld(RB2_PR1 + A1mm, OWN);
+        const double ow = ld(RB2_PR2 + A2m, OWN);     // the pair's first-colour cell of R2 at q-2
+        double wdn = ld(RB2_PR2 + A2m, DNo), wup = ld(RB2_PR2 + A2m, UPo);
+        const double wsd = ld(RB2_PR2 + A2m, SD);
+        double zm2 = ld(RB2_PR2 + A2mm, OWN);
+        __builtin_amdgcn_sched_barrier(0);
         // ---- S2: Y1_q, second colour (component e) from R1 ----
-        const bool pin0 = (q >= 1 && q <= nzi);
-        const double r1c = L.r1[A1c][r][c];  // the pair's first-colour cell of R1_q
-        const double r1m = L.r1[A1m][r][c];  // ... of R1_{q-1} (= Y1' there)
         double y1v;
         {
-            const double rdn = L.r1[A1c][rlo][c], rup = L.r1[A1c][rhi][c];
-            const double rsd = (e == 0) ? L.r1[A1c][r][cm] : L.r1[A1c][r][cp];
-            const double sx = (e == 0) ? r1c + rsd : rsd + r1c;
-            const double v = rb2_sor<APX>(rc, comp(Xm, e), sx, rup + rdn, r1v + r1m,
+            const double sx = (e == 0) ? r1c + r1sd : r1sd + r1c;
+            const double v = rb2_sor<APX>(rc, comp(Xm, e), sx, r1up + r1dn, r1v + r1m,
                                           comp(br[B0], e));
-            y1v = (pin0 && (e == 0 ? in0 : in1)) ? v : comp(Xm, e);
-            if (q >= kb && q < ke) cert(e == 0 ? own0 : own1, y1v);
+            y1v = (pin0 && ine) ? v : comp(Xm, e);
+            cert(ok0 && owe, y1v);
+            pin();
         }
         __builtin_amdgcn_sched_barrier(0);
         // ---- S3: R2_{q-1} from Y1' (+ L-inf residual of Y1' at plane q-1) ----
-        const int qc = q - 1;
-        const bool pinm = (qc >= 1 && qc <= nzi);
-        const double y1mm = L.y1[AYmm][r][c];  // Y1' second-colour cell at q-2 (= R2 there)
         double r2v;
         {
-            const double cen = r1m;                 // Y1' first-colour cell at q-1
-            const double ob = L.y1[AYm][r][c];      // the pair's second-colour cell at q-1
-            double ydn = L.y1[AYm][rlo][c], yup = L.y1[AYm][rhi][c];
-            const double ysd = (e == 0) ? L.y1[AYm][r][cm] : L.y1[AYm][r][cp];
-            double zm = y1mm, zp = y1v;
-            if (qc == 1) zm = cen;
-            if (qc == nzi) zp = cen;
-            if (fdn) ydn = cen;
-            if (fup) yup = cen;
+            const double cen = r1m;  // Y1' first-colour cell at q-1
+            const double zm = (qc == 1) ? cen : y1mm;
+            const double zp = (qc == nzi) ? cen : y1v;
+            ydn = fdn ? cen : ydn;
+            yup = fup ? cen : yup;
             double lf, rt;
             if (e == 0) {
                 lf = ysd;
@@ -324,55 +374,45 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             const double sx = rt + lf, sy = yup + ydn, sz = zp + zm;
             const double2 bm = br[Bm1];
             const double v = rb2_sor<APX>(rc, cen, sx, sy, sz, comp(bm, e));
-            r2v = (pinm && (e == 0 ? in0 : in1)) ? v : cen;
-            if (qc >= kb && qc < ke) {
-                // the residual of Y1' at plane q-1: cell e (first colour)
-                // shares the update's sums; cell 1-e (second colour, value ob)
-                // reads the first-colour cells of Y1' = R1 at q-1
-                const double cb = ob;
-                double rdn = L.r1[A1m][rlo][c], rup = L.r1[A1m][rhi][c];
-                const double rsd = (e == 0) ? L.r1[A1m][r][cp] : L.r1[A1m][r][cm];
-                double wm = L.r1[A1mm][r][c], wp = r1c;
-                if (qc == 1) wm = cb;
-                if (qc == nzi) wp = cb;
-                if (fdn) rdn = cb;
-                if (fup) rup = cb;
-                double lf2, rt2;
-                if (e == 0) {  // cell 1 (.y): left own .x (first colour), right pair c+1 .x
-                    lf2 = f1l ? cb : cen;
-                    rt2 = f1r ? cb : rsd;
-                } else {       // cell 0 (.x): left pair c-1 .y, right own .y
-                    lf2 = rsd;
-                    rt2 = f0r ? cb : cen;
-                }
-                double ae, ab;
-                if constexpr (APX) {
-                    ae = rb2_res_apx(cf, cen, sx, sy, sz, comp(bm, e));
-                    ab = rb2_res_apx(cf, cb, rt2 + lf2, rup + rdn, wp + wm, comp(bm, 1 - e));
-                } else {
-                    ae = res1(rc, DivC{}, cen, lf, rt, ydn, yup, zm, zp, comp(bm, e));
-                    ab = res1(rc, DivC{}, cb, lf2, rt2, rdn, rup, wm, wp, comp(bm, 1 - e));
-                }
-                const bool oe = (e == 0) ? own0 : own1, ob_ = (e == 0) ? own1 : own0;
-                if (oe && ae > mY) mY = ae;
-                if (ob_ && ab > mY) mY = ab;
-                cert(oe, r2v);
+            r2v = (pinm && ine) ? v : cen;
+            // the residual of Y1' at plane q-1: cell e (first colour) shares the
+            // update's sums; cell 1-e (second colour, value ob) reads the
+            // first-colour cells of Y1' = R1 at q-1
+            const double cb = ob;
+            const double wm = (qc == 1) ? cb : wm1;
+            const double wp = (qc == nzi) ? cb : r1c;
+            qdn = fdn ? cb : qdn;
+            qup = fup ? cb : qup;
+            double lf2, rt2;
+            if (e == 0) {  // cell 1 (.y): left own .x (first colour), right pair c+1 .x
+                lf2 = f1l ? cb : cen;
+                rt2 = f1r ? cb : qsd;
+            } else {       // cell 0 (.x): left pair c-1 .y, right own .y
+                lf2 = qsd;
+                rt2 = f0r ? cb : cen;
             }
+            double ae, ab;
+            if constexpr (APX) {
+                ae = rb2_res_apx(cf, cen, sx, sy, sz, comp(bm, e));
+                ab = rb2_res_apx(cf, cb, rt2 + lf2, qup + qdn, wp + wm, comp(bm, 1 - e));
+            } else {
+                ae = res1(rc, DivC{}, cen, lf, rt, ydn, yup, zm, zp, comp(bm, e));
+                ab = res1(rc, DivC{}, cb, lf2, rt2, qdn, qup, wm, wp, comp(bm, 1 - e));
+            }
+            mY = umax(okc && owe, ae, mY);
+            mY = umax(okc && owb, ab, mY);
+            cert(okc && owe, r2v);
+            pin();
         }
         __builtin_amdgcn_sched_barrier(0);
         // ---- S4: Y2_{q-2}, second colour from R2 -> stored ----
-        const int qd = q - 2;
+        double2 out;
         {
-            const bool pind = (qd >= 1 && qd <= nzi);
-            const double cen = y1mm;             // Y1' second-colour cell at q-2
-            const double ow = L.r2[A2m][r][c];   // the pair's first-colour cell of R2 at q-2
-            double wdn = L.r2[A2m][rlo][c], wup = L.r2[A2m][rhi][c];
-            const double wsd = (e == 0) ? L.r2[A2m][r][cm] : L.r2[A2m][r][cp];
-            double zm = L.r2[A2mm][r][c], zp = r2v;
-            if (qd == 1) zm = cen;
-            if (qd == nzi) zp = cen;
-            if (fdn) wdn = cen;
-            if (fup) wup = cen;
+            const double cen = y1mm;  // Y1' second-colour cell at q-2
+            const double zm = (qd == 1) ? cen : zm2;
+            const double zp = (qd == nzi) ? cen : r2v;
+            wdn = fdn ? cen : wdn;
+            wup = fup ? cen : wup;
             double lf, rt;
             if (e == 0) {
                 lf = wsd;
@@ -382,36 +422,38 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 rt = f1r ? cen : wsd;
             }
             const double v = rb2_sor<APX>(rc, cen, rt + lf, wup + wdn, zp + zm, bq2);
-            const double y2v = (pind && (e == 0 ? in0 : in1)) ? v : cen;
-            if (qd >= kb && qd < ke) {
-                cert(e == 0 ? own0 : own1, y2v);
-                double2 out = (e == 0) ? make_double2(y2v, ow) : make_double2(ow, y2v);
-                // the Neumann shell folded into the stores (as k_rb1)
-                if (nrole & 1) out.x = out.y;
-                if (nrole & 2) out.y = out.x;
-                if (nrole & 8) {
-                    auto put = [&](long long base) __attribute__((always_inline)) {
-                        st2v<FL>(Y, base, out);
-                        if (nrole & 4) Y[base + 2] = out.y;
-                        if (BND && (j == 1 || j == g.ny - 2)) {
-                            const long long b2 = base + (j == 1 ? -g.px : g.px);
-                            st2v<FL>(Y, b2, out);
-                            if (nrole & 4) Y[b2 + 2] = out.y;
-                        }
-                    };
-                    const long long base = (long long)qd * g.ps + col;
-                    put(base);
-                    if (qd == 1) put(base - g.ps);
-                    if (qd == nzi) put(base + g.ps);
-                }
+            const double y2v = (pind && ine) ? v : cen;
+            cert(okd && owe, y2v);
+            pin();
+            out = (e == 0) ? make_double2(y2v, ow) : make_double2(ow, y2v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- publish for step q + 1, then store Y2 ----
+        st(RB2_PX + 2 * LX2, Xp.x);
+        st(RB2_PX + 2 * LX2 + 1, Xp.y);
+        st(RB2_PR1 + A1n, r1v);
+        st(RB2_PY1 + AYn, y1v);
+        st(RB2_PR2 + A2n, r2v);
+        if (okd) {
+            // the Neumann shell folded into the stores (as k_rb1)
+            if (nrole & 1) out.x = out.y;
+            if (nrole & 2) out.y = out.x;
+            if (nrole & 8) {
+                auto put = [&](double* yp) __attribute__((always_inline)) {
+                    st2v<FL>(yp, col, out);
+                    if (nrole & 4) yp[col + 2] = out.y;
+                    if (BND && (j == 1 || j == g.ny - 2)) {
+                        const int c2 = col + (j == 1 ? -px : px);
+                        st2v<FL>(yp, c2, out);
+                        if (nrole & 4) yp[c2 + 2] = out.y;
+                    }
+                };
+                double* yq = Y + (long long)qd * g.ps;
+                put(yq);
+                if (qd == 1) put(yq - g.ps);
+                if (qd == nzi) put(yq + g.ps);
             }
         }
-        // ---- publish for step q + 1 ----
-        L.xs[LX2][r][0][c] = Xp.x;
-        L.xs[LX2][r][1][c] = Xp.y;
-        L.r1[A1n][r][c] = r1v;
-        L.y1[AYn][r][c] = y1v;
-        L.r2[A2n][r][c] = r2v;
     };
     // E(q) = ((j + q + kofs) & 1) == 0, wave-uniform (rows r and r + 16 share it)
     const bool E0 = __builtin_amdgcn_readfirstlane(((j + q0 + g.kofs) & 1) == 0 ? 1 : 0) != 0;

@@ -148,7 +148,8 @@ typedef enum {
     HIP_KT_ALLREDUCE = 13, /* Z-slabs: RCCL all-reduce of a CG dot (+ finish kernel); the
                               device-mailbox reduction runs inside the sweep instead */
     HIP_KT_CG_SMALL = 14,  /* small grids: the whole CG solve in one cooperative launch */
-    HIP_KT_COUNT = 15
+    HIP_KT_RELAX2 = 15,    /* RB-SOR: one sweep of TWO iterations (k_rb2, one device, 3-D) */
+    HIP_KT_COUNT = 16
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);

@@ -43,10 +43,13 @@ def main():
         kt = ctx.timing()
         ctx.enable_timing(False)
         ctx.close()
-        relax, res = kt["relax"], kt["residual"]
+        # one-iteration sweeps (k_rb1 / k_rx) and two-iteration sweeps (k_rb2)
+        relax = (kt["relax"][0] + kt["relax2"][0], kt["relax"][1] + kt["relax2"][1])
+        res = kt["residual"]
         per_it = (relax[0] + res[0]) / iters
         print(json.dumps({"method": name, "grid": [nx, ny, nz], "iters": st.iterations, "status": s,
-                          "rb_variant": os.environ.get("CFD_HIP_RB_VARIANT"),
+                          "rb2": os.environ.get("CFD_HIP_RB2"),
+                          "sweeps_1it": kt["relax"][1], "sweeps_2it": kt["relax2"][1],
                           "iter_ms_kernels": round(per_it, 4),
                           "relax_ms": round(relax[0] / iters, 4),
                           "residual_ms": round(res[0] / max(res[1], 1), 4),
