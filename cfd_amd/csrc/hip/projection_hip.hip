@@ -508,6 +508,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     }
     constexpr int FLR = SW_NT_STORE | SW_PREFETCH | SW_EDGE1;
     const SGeo& g2 = c->r2geo;
+    const int xmap = getenv("CFD_HIP_RB2_XMAP") ? atoi(getenv("CFD_HIP_RB2_XMAP")) : 0;
     const unsigned nb2 = (unsigned)(g2.tiles_x * g2.tiles_y * g2.tiles_z);
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
                           rel_tol, abs_tol, max_iter, 1);
@@ -540,12 +541,12 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
                     hipExtLaunchKernelGGL((k_rb2<true, FLR>), dim3(nb2), dim3(1024), 0, c->stream,
                                           c->ta, c->tb, 0, g2, cf, (const double*)bx, by,
                                           (const double*)c->rhs, c->rxst, c->partials,
-                                          c->counter, cur, certx);
+                                          c->counter, cur, certx, xmap);
                 else
                     hipExtLaunchKernelGGL((k_rb2<false, FLR>), dim3(nb2), dim3(1024), 0,
                                           c->stream, c->ta, c->tb, 0, g2, cf, (const double*)bx,
                                           by, (const double*)c->rhs, c->rxst, c->partials,
-                                          c->counter, cur, certx);
+                                          c->counter, cur, certx, xmap);
             }, cur);
             log.push_back({cur, 2, bx, by});
             cur += 2;

@@ -483,10 +483,15 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
                                                        double* __restrict__ Y,
                                                        const double* __restrict__ rhs,
                                                        RxState* st, double* partials,
-                                                       unsigned* counter, int s, int certx) {
+                                                       unsigned* counter, int s, int certx,
+                                                       int xmap) {
     __shared__ Rb2Lds L;
     if (st->done) return;
-    const int t = blockIdx.x;
+    // tile order: xmap = 1 gives each XCD a contiguous range of tiles
+    // (xcd_tile), so the halo rows and columns a tile shares with its x / y
+    // neighbours are fetched once into that XCD's L2 by whichever of the
+    // concurrently running neighbours gets there first
+    const int t = xmap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int tx = t % g.tiles_x;
     const int rest = t / g.tiles_x;
     const int ty = rest % g.tiles_y;

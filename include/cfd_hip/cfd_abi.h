@@ -37,6 +37,16 @@ extern "C" {
 #define CFD_HIP_EXPORT __attribute__((visibility("default")))
 #endif
 
+#ifdef CFD_HIP_REFERENCE_TYPES
+/* Inside a reference build: the reference's own
+ * headers define these types, with the layouts restated below. */
+#include "cfd/core/cfd_status.h"
+#include "cfd/core/grid.h"
+#include "cfd/boundary/boundary_conditions.h"
+#include "cfd/solvers/navier_stokes_solver.h"
+#include "cfd/solvers/poisson_solver.h"
+#else
+
 /* ---- status codes (values are part of the ABI) ------------------------- */
 typedef enum {
     CFD_SUCCESS = 0,
@@ -312,6 +322,8 @@ struct poisson_solver {
     poisson_solver_iterate_func iterate;
     poisson_solver_apply_bc_func apply_bc;
 };
+
+#endif /* CFD_HIP_REFERENCE_TYPES */
 
 #ifdef __cplusplus
 }
