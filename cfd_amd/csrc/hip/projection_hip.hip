@@ -500,12 +500,18 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     cf.k2 = 2.0 * (rc.rdx2 + rc.rdy2 + rc.inv_dz2);
     cf.kb = rc.rdx2 + rc.rdy2 + rc.inv_dz2;
     cf.escale = 1.0;
-    cf.elim = -800.0;
+    cf.mlim = 0x1p800;
+    cf.slow = -899;
+    cf.pad = 0;
     if (const char* e = getenv("CFD_HIP_RB2_TEST")) {  // tests: force the host paths
         const int v = atoi(e);
         if (v == 1) cf.escale = 1e300;  // every approximate decision ambiguous
-        if (v == 2) cf.elim = 4096.0;   // every sweep uncertified
+        if (v == 2) cf.mlim = 0.0;      // every sweep uncertified
+        if (v == 3) cf.slow = 100000;   // every SOR update in the reference's arithmetic
     }
+    // the fast division's range argument (rb2.hpp rb2_sorc) needs 1 <= 1/d^2 <= 2^60
+    if (!(rc.rdx2 >= 1.0 && rc.rdy2 >= 1.0 && rc.rdx2 <= 0x1p60 && rc.rdy2 <= 0x1p60))
+        apx = false;
     constexpr int FLR = SW_NT_STORE | SW_PREFETCH | SW_EDGE1;
     const SGeo& g2 = c->r2geo;
     const int xmap = getenv("CFD_HIP_RB2_XMAP") ? atoi(getenv("CFD_HIP_RB2_XMAP")) : 0;
@@ -1201,7 +1207,10 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             r2.xofs = 0;
             r2.tiles_x = (int)((nx - 1 + RB2_OX - 1) / RB2_OX);
             r2.tiles_y = (int)((ny - 1 + RB2_OY - 1) / RB2_OY);
-            r2.kc = 64;
+            // 128-plane z runs: the 6-plane pipeline fill is 4.7 % of a run
+            // (1024^2 x 512: 2.16 -> 2.05 ms per iteration against 64;
+            // 32: 2.34, profiles/r04_rb2_kc.jsonl)
+            r2.kc = 128;
             if (const char* e = getenv("CFD_HIP_RB2_KC")) r2.kc = std::max(1, atoi(e));
             while (r2.kc > 4 &&
                    (long long)r2.tiles_x * r2.tiles_y * ((nint_k + r2.kc - 1) / r2.kc) < 512)

@@ -75,9 +75,12 @@ struct Rb2Coef {
     double k2;   // 2 (RN(1/dx2) + RN(1/dy2) + inv_dz2): the centre weight of the approximation
     double kb;   // 1/dx2 + 1/dy2 + inv_dz2 (error bound)
     // test knobs (CFD_HIP_RB2_TEST): escale multiplies the residual bound
-    // (1e300: every decision ambiguous), elim is the least certified
-    // exponent (-800; 4096: every sweep uncertified)
-    double escale, elim;
+    // (1e300: every decision ambiguous); mlim is the largest certified
+    // |value| (2^800; 0: every sweep uncertified); slow is the least binary
+    // exponent of a divided neighbour sum the fast division takes (-899;
+    // 100000: every SOR update recomputed in the reference's arithmetic)
+    double escale, mlim;
+    int slow, pad;
 };
 
 // LDS of one k_rb2 workgroup (148 KB): X by plane parity, and the one-colour
@@ -113,11 +116,19 @@ __device__ __forceinline__ double rb2_div(double a, double d, double r) {
 // sz = above + below (linear_solver_redblack.c:103-112 order, as sor1)
 template <bool APX>
 __device__ __forceinline__ double rb2_sor(const RelaxCoef& rc, double vc, double sx, double sy,
-                                          double sz, double vb) {
-    const double pn = -(vb - rb2_div<APX>(sx, rc.dx2, rc.rdx2) -
-                        rb2_div<APX>(sy, rc.dy2, rc.rdy2) - sz * rc.inv_dz2) *
-                      rc.inv_factor;
+                                          double sz, double vb, double* tout = nullptr) {
+    const double t = vb - rb2_div<APX>(sx, rc.dx2, rc.rdx2) - rb2_div<APX>(sy, rc.dy2, rc.rdy2) -
+                     sz * rc.inv_dz2;
+    if (tout) *tout = t;
+    const double pn = -t * rc.inv_factor;
     return vc + rc.omega * (pn - vc);
+}
+
+// the approximate residual of the cell an update just touched, from the
+// update's own t = b - sx/dx^2 - sy/dy^2 - sz/dz^2 (lap - b = -t - k2 c):
+// one FMA, within the same bound as rb2_res_apx
+__device__ __forceinline__ double rb2_res_from_t(const Rb2Coef& cf, double c, double t) {
+    return fabs(fma(c, -cf.k2, -t));
 }
 
 // approximate |lap(x) - rhs| from the neighbour sums (see the header)
@@ -129,6 +140,29 @@ __device__ __forceinline__ double rb2_res_apx(const Rb2Coef& cf, double c, doubl
 
 // the binary exponent of v as frexp gives it (0 for zero)
 __device__ __forceinline__ int rb2_exp(double v) { return __builtin_amdgcn_frexp_exp(v); }
+
+// One SOR update, APX: the fast divisions, with their range test folded into
+// ONE wave-uniform branch per update. The fast quotient is correctly rounded
+// for |a r| in [2^-900, 2^900] or a = 0 (divz); the sweep certifies |v| <=
+// 2^800 for every value (so |sx|, |sy| <= 2^801, and 1 <= 1/d^2 <= 2^60 is
+// checked on the host), and here a wave in which some neighbour sum is
+// nonzero with |sum| < 2^-900 (binary exponent < -899: the zero-valued front
+// of a solve from a zero guess leaves such values) recomputes the update with
+// divc. Either way the value is the reference's.
+template <bool APX>
+__device__ __forceinline__ double rb2_sorc(const RelaxCoef& rc, int slow, double vc, double sx,
+                                           double sy, double sz, double vb,
+                                           double* tout = nullptr) {
+    if constexpr (!APX) {
+        return rb2_sor<false>(rc, vc, sx, sy, sz, vb, tout);
+    } else {
+        double v = rb2_sor<true>(rc, vc, sx, sy, sz, vb, tout);
+        const int ex = min(rb2_exp(sx), rb2_exp(sy));
+        if (__builtin_amdgcn_ballot_w64(ex < slow) != 0)
+            v = rb2_sor<false>(rc, vc, sx, sy, sz, vb, tout);
+        return v;
+    }
+}
 
 // The decision of the common loop for iterate `it` >= 1 (check_interval 1)
 // from an approximate residual maximum m with bound E; false = ambiguous.
@@ -237,14 +271,22 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     // X_{q0+1} into the X slot step q0 reads: LDS slots count planes from q0
     st(RB2_PX + 2, xr[1].x);
     st(RB2_PX + 3, xr[1].y);
+    // the one-cell pad of every plane is never written by a step; zero it, so
+    // that what halo lanes compute from it stays ordinary values (a stale
+    // denormal there would send waves to rb2_sorc's recompute for nothing)
+    for (int e = threadIdx.x; e < 16 * 2 * (RB2_LP + RB2_TR); e += 1024) {
+        const int pl = e / (2 * (RB2_LP + RB2_TR)), q = e % (2 * (RB2_LP + RB2_TR));
+        const int idx = q < 2 * RB2_LP ? (q < RB2_LP ? q : (RB2_TR + 1) * RB2_LP + q - RB2_LP)
+                                       : ((q - 2 * RB2_LP) / 2 + 1) * RB2_LP +
+                                             ((q & 1) ? RB2_LP - 1 : 0);
+        L.pl[pl][idx] = 0.0;
+    }
     // certification of one value (APX): branch-free, so the step stays one
     // basic block and its LDS reads can be scheduled ahead of the arithmetic
     auto cert = [&](bool ok, double v) __attribute__((always_inline)) {
         if constexpr (APX) {
             const double av = fabs(v);
             M = (ok && av > M) ? av : M;
-            const int ev = rb2_exp(v);
-            emin = (ok && ev < emin) ? ev : emin;
         }
     };
     auto umax = [](bool ok, double a, double m) __attribute__((always_inline)) {
@@ -255,7 +297,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     // to the loop's back edge, where their operands no longer fit in VGPRs
     auto pin = [&]() __attribute__((always_inline)) {
         asm volatile("" : "+v"(mX), "+v"(mY));
-        if constexpr (APX) asm volatile("" : "+v"(M), "+v"(emin));
+        if constexpr (APX) asm volatile("" : "+v"(M));
     };
     const int nzi = g.nz - 2;  // last interior plane
     auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
@@ -306,19 +348,21 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         // neighbour sums (right + left, up + down, above + below) of both cells
         const double sx0 = Xc.y + xlp, sy0 = xhi.x + xlo.x, sz0 = Xp.x + Xm.x;
         const double sx1 = xrp + Xc.x, sy1 = xhi.y + xlo.y, sz1 = Xp.y + Xm.y;
-        double r1v;
+        double r1v, t1;
         if (e == 0) {
-            const double v = rb2_sor<APX>(rc, Xc.x, sx0, sy0, sz0, b1.x);
+            const double v = rb2_sorc<APX>(rc, cf.slow, Xc.x, sx0, sy0, sz0, b1.x, &t1);
             r1v = (pin1 && in0) ? v : Xc.x;
         } else {
-            const double v = rb2_sor<APX>(rc, Xc.y, sx1, sy1, sz1, b1.y);
+            const double v = rb2_sorc<APX>(rc, cf.slow, Xc.y, sx1, sy1, sz1, b1.y, &t1);
             r1v = (pin1 && in1) ? v : Xc.y;
         }
         {
             double a0, a1;
             if constexpr (APX) {
-                a0 = rb2_res_apx(cf, Xc.x, sx0, sy0, sz0, b1.x);
-                a1 = rb2_res_apx(cf, Xc.y, sx1, sy1, sz1, b1.y);
+                a0 = (e == 0) ? rb2_res_from_t(cf, Xc.x, t1)
+                              : rb2_res_apx(cf, Xc.x, sx0, sy0, sz0, b1.x);
+                a1 = (e == 1) ? rb2_res_from_t(cf, Xc.y, t1)
+                              : rb2_res_apx(cf, Xc.y, sx1, sy1, sz1, b1.y);
             } else {
                 a0 = res1(rc, DivC{}, Xc.x, xlp, Xc.y, xlo.x, xhi.x, Xm.x, Xp.x, b1.x);
                 a1 = res1(rc, DivC{}, Xc.y, Xc.x, xrp, xlo.y, xhi.y, Xm.y, Xp.y, b1.y);
@@ -348,7 +392,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         double y1v;
         {
             const double sx = (e == 0) ? r1c + r1sd : r1sd + r1c;
-            const double v = rb2_sor<APX>(rc, comp(Xm, e), sx, r1up + r1dn, r1v + r1m,
+            const double v = rb2_sorc<APX>(rc, cf.slow, comp(Xm, e), sx, r1up + r1dn, r1v + r1m,
                                           comp(br[B0], e));
             y1v = (pin0 && ine) ? v : comp(Xm, e);
             cert(ok0 && owe, y1v);
@@ -373,7 +417,8 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             }
             const double sx = rt + lf, sy = yup + ydn, sz = zp + zm;
             const double2 bm = br[Bm1];
-            const double v = rb2_sor<APX>(rc, cen, sx, sy, sz, comp(bm, e));
+            double t3;
+            const double v = rb2_sorc<APX>(rc, cf.slow, cen, sx, sy, sz, comp(bm, e), &t3);
             r2v = (pinm && ine) ? v : cen;
             // the residual of Y1' at plane q-1: cell e (first colour) shares the
             // update's sums; cell 1-e (second colour, value ob) reads the
@@ -393,7 +438,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             }
             double ae, ab;
             if constexpr (APX) {
-                ae = rb2_res_apx(cf, cen, sx, sy, sz, comp(bm, e));
+                ae = rb2_res_from_t(cf, cen, t3);
                 ab = rb2_res_apx(cf, cb, rt2 + lf2, qup + qdn, wp + wm, comp(bm, 1 - e));
             } else {
                 ae = res1(rc, DivC{}, cen, lf, rt, ydn, yup, zm, zp, comp(bm, e));
@@ -421,7 +466,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 lf = f1l ? cen : ow;
                 rt = f1r ? cen : wsd;
             }
-            const double v = rb2_sor<APX>(rc, cen, rt + lf, wup + wdn, zp + zm, bq2);
+            const double v = rb2_sorc<APX>(rc, cf.slow, cen, rt + lf, wup + wdn, zp + zm, bq2);
             const double y2v = (pind && ine) ? v : cen;
             cert(okd && owe, y2v);
             pin();
@@ -580,7 +625,7 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
         }
         __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (APX) {
-            if (tE < cf.elim || !(tM <= 0x1p800)) {
+            if (!(tM <= cf.mlim)) {
                 st->done = 1;
                 st->status = ST_RB2_UNCERT;
                 st->res_it = s;

@@ -10,6 +10,8 @@ Every host path of relax_solve_rb2 is forced in turn:
                              resolves each iterate's residual exactly
   + CFD_HIP_RB2_TEST = 2     every sweep uncertified: the host reruns with
                              one iteration per sweep (k_rb1)
+  + CFD_HIP_RB2_TEST = 3     every SOR update takes the in-kernel exact
+                             recompute (the path of tiny neighbour sums)
 and the loop stops on both the input and the middle iterate of a sweep
 (odd and even iteration counts, converged and capped)."""
 import numpy as np
@@ -33,7 +35,7 @@ SHAPES = [
     ((120, 49, 33), dict(max_iterations=2)),
     ((120, 49, 33), dict(max_iterations=1)),
 ]
-MODES = [("2", "0"), ("1", "0"), ("1", "1"), ("1", "2")]
+MODES = [("2", "0"), ("1", "0"), ("1", "1"), ("1", "2"), ("1", "3")]
 
 
 def _solve(shape, kw):
@@ -81,3 +83,34 @@ def test_rb2_stops_on_both_iterates(hip_lib, monkeypatch):
         if sto.status == 0:
             seen.add(sto.iterations % 2)
     assert seen == {0, 1}, seen
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("iters", [30, 31])
+def test_rb2_tiny_front_bitwise(hip_lib, monkeypatch, mode, iters):
+    """A solve from x0 = 0 with a right-hand side of 1e-262 in one corner and
+    zero tolerances: the iterate's front decays to values far below 2^-899
+    (about 22 000 cells at 30 iterations), whose neighbour sums the fast
+    division must not take -- those waves recompute their update exactly
+    (rb2.hpp rb2_sorc); bitwise against the oracle, capped at an even and an
+    odd iteration."""
+    monkeypatch.setenv("CFD_HIP_RB2", mode)
+    nx, ny, nz = 96, 80, 70
+    rhs = np.zeros((nz, ny, nx))
+    rhs[2:6, 2:6, 2:6] = 1e-262
+    x0 = np.zeros_like(rhs)
+    d = 1.0 / (nx - 1)
+    prm = oracle.poisson_params(max_iterations=iters, tolerance=0.0, absolute_tolerance=0.0)
+    xo = x0.copy()
+    so, sto = oracle.redblack_solve(xo, rhs, d, d, d, prm)
+    nzv = np.abs(xo[xo != 0])
+    assert int((nzv < 2.0 ** -899).sum()) > 1000  # the front really is that small
+    ctx = api.HipProjection(nx, ny, nz)
+    xh = x0.copy()
+    sh, sth = ctx.poisson_solve(A.HIP_POISSON_REDBLACK, xh, rhs, d, d, d, prm)
+    ctx.close()
+    assert sh == so
+    assert (sth.iterations, sth.status) == (sto.iterations, sto.status)
+    assert sth.initial_residual == sto.initial_residual
+    assert sth.final_residual == sto.final_residual
+    np.testing.assert_array_equal(xh, xo)
