@@ -42,12 +42,13 @@
 // Both are certified per sweep, so every decision and every stored value is
 // the reference's bit for bit:
 //  - range: the fast quotient is the correctly rounded a/d whenever |a/d| is
-//    in [2^-900, 2^900] or a = +-0 (divc / divz, tools/divc_check.c). Every
-//    value the sweep reads or writes is checked: its binary exponent >= -800
-//    (or zero) and |v| <= 2^800, which bounds every nonzero neighbour sum to
-//    [2^-852, 2^801] and the quotients into that interval for 1 <= 1/d <=
-//    2^40. A sweep that fails the check stops the loop (ST_RB2_UNCERT) and
-//    the host reruns its iterations with k_rb1.
+//    in [2^-900, 2^900] or a = +-0 (divc / divz, tools/divc_check.c). The
+//    sweep certifies M = max |v| <= 2^800 over every value it reads or
+//    writes (so every neighbour sum is at most 2^801; 1 <= 1/d <= 2^60 is
+//    checked on the host); a sweep that fails it stops the loop
+//    (ST_RB2_UNCERT) and the host reruns its iterations with k_rb1. The
+//    lower end is tested per update (rb2_sorc): a wave holding a nonzero
+//    neighbour sum below 2^-900 recomputes that update with divc.
 //  - residuals: both the reference's value and the approximation are within
 //    8u (4 M K + B) of the exact residual (u = 2^-53, M = max |v| over the
 //    sweep's values, K = 1/dx^2 + 1/dy^2 + 1/dz^2, B = max |rhs|); the loop
@@ -141,6 +142,25 @@ __device__ __forceinline__ double rb2_res_apx(const Rb2Coef& cf, double c, doubl
 // the binary exponent of v as frexp gives it (0 for zero)
 __device__ __forceinline__ int rb2_exp(double v) { return __builtin_amdgcn_frexp_exp(v); }
 
+// running maxima in one instruction: max(m, a) and max(m, |a|) (a quiet NaN
+// operand is dropped, as the compare-and-select form drops it); written out
+// because fmax on a loop-carried value costs a canonicalize per use
+__device__ __forceinline__ double rb2_vmax(double m, double a) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(m), "v"(a));
+    return r;
+}
+__device__ __forceinline__ double rb2_vmax_abs(double m, double a) {
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(a));
+    return r;
+}
+__device__ __forceinline__ double rb2_max_abs2(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // One SOR update, APX: the fast divisions, with their range test folded into
 // ONE wave-uniform branch per update. The fast quotient is correctly rounded
 // for |a r| in [2^-900, 2^900] or a = 0 (divz); the sweep certifies |v| <=
@@ -209,7 +229,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                                           const double* __restrict__ X, double* __restrict__ Y,
                                           const double* __restrict__ rhs, int c, int r, int i0,
                                           int j, int kb, int ke, int certx, double& mX,
-                                          double& mY, double& M, int& emin) {
+                                          double& mY, double& M) {
     const RelaxCoef& rc = cf.rc;
     // LDS addressing: two per-lane bases (planes 0-7 and 8-15), each at the
     // lane's cell minus one row and one column, so every operand is a
@@ -218,7 +238,12 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     double* const Lb0 = &L.pl[0][r * RB2_LP + c];
     double* const Lb1 = &L.pl[8][r * RB2_LP + c];
     constexpr int OWN = RB2_LP + 1, LF = RB2_LP, RT = RB2_LP + 2, DNo = 1, UPo = 2 * RB2_LP + 1;
+    // every read stays a ds_read_b64 (2 LDS cycles per wave): the compiler
+    // would pair same-plane reads into ds_read2_b64, which takes 8. A
+    // scheduling barrier that lets every instruction class cross it still
+    // ends the pairing pass's search window.
     auto ld = [&](int plane, int d) __attribute__((always_inline)) -> double {
+        __builtin_amdgcn_sched_barrier(0x7ff);
         return plane < 8 ? Lb0[plane * RB2_LS + d] : Lb1[(plane - 8) * RB2_LS + d];
     };
     auto st = [&](int plane, double v) __attribute__((always_inline)) {
@@ -300,9 +325,29 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         if constexpr (APX) asm volatile("" : "+v"(M));
     };
     const int nzi = g.nz - 2;  // last interior plane
-    auto step = [&](auto Ec, auto Pc, int q) __attribute__((always_inline)) {
+    const double cxf = certx ? 1.0 : 0.0;
+    // ZB: a step at the ends of the march or next to a z face (range and
+    // face tests per plane); the steady steps between take every stage in
+    // range and no z face, so those tests fold away, and in an interior tile
+    // (!BND) the maxima run over every lane unmasked: the owned-lane mask of
+    // the residuals is applied once after the march, and the certification
+    // bound may include halo lanes' values (finite: computed from the
+    // planes this march wrote, the zeroed pads and clamped loads)
+    auto step = [&](auto Ec, auto Pc, auto Zc, int q) __attribute__((always_inline)) {
         constexpr bool E = decltype(Ec)::value;
         constexpr int P = decltype(Pc)::value;
+        constexpr bool ZB = decltype(Zc)::value;
+        auto rmax = [&](double& m, bool ok, bool ow, double a) __attribute__((always_inline)) {
+            if constexpr (!ZB && !BND) m = rb2_vmax(m, a);
+            else m = umax(ok && ow, a, m);
+        };
+        auto certv = [&](bool ok, bool ow, double v) __attribute__((always_inline)) {
+            if constexpr (!ZB) {
+                if constexpr (APX) M = rb2_vmax_abs(M, v);
+            } else {
+                cert(ok && ow, v);
+            }
+        };
         constexpr int e = E ? 0 : 1;  // the component every update of this step touches
         // register rings (X, rhs): slot of plane p = (P + p - q + off) & 3
         constexpr int X0 = P & 3, X1 = (P + 1) & 3, X2 = (P + 2) & 3, X3 = (P + 3) & 3;
@@ -321,10 +366,13 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         br[B2] = ldr(q + 2);
         __syncthreads();
         const int qa = q + 1, qc = q - 1, qd = q - 2;
-        const bool pin1 = (qa >= 1 && qa <= nzi), pin0 = (q >= 1 && q <= nzi);
-        const bool pinm = (qc >= 1 && qc <= nzi), pind = (qd >= 1 && qd <= nzi);
-        const bool oka = (qa >= kb && qa < ke), ok0 = (q >= kb && q < ke);
-        const bool okc = (qc >= kb && qc < ke), okd = (qd >= kb && qd < ke);
+        const bool pin1 = !ZB || (qa >= 1 && qa <= nzi), pin0 = !ZB || (q >= 1 && q <= nzi);
+        const bool pinm = !ZB || (qc >= 1 && qc <= nzi), pind = !ZB || (qd >= 1 && qd <= nzi);
+        const bool oka = !ZB || (qa >= kb && qa < ke), ok0 = !ZB || (q >= kb && q < ke);
+        const bool okc = !ZB || (qc >= kb && qc < ke), okd = !ZB || (qd >= kb && qd < ke);
+        // z faces next to the stages of iteration 2 (their Neumann copies)
+        const bool zc1 = ZB && qc == 1, zcn = ZB && qc == nzi;
+        const bool zd1 = ZB && qd == 1, zdn = ZB && qd == nzi;
         const bool ine = (e == 0) ? in0 : in1;
         const bool owe = (e == 0) ? own0 : own1, owb = (e == 0) ? own1 : own0;
         // ---- LDS operands of S1 and S2 ----
@@ -367,11 +415,18 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 a0 = res1(rc, DivC{}, Xc.x, xlp, Xc.y, xlo.x, xhi.x, Xm.x, Xp.x, b1.x);
                 a1 = res1(rc, DivC{}, Xc.y, Xc.x, xrp, xlo.y, xhi.y, Xm.y, Xp.y, b1.y);
             }
-            mX = umax(oka && own0, a0, mX);
-            mX = umax(oka && own1, a1, mX);
-            cert(oka && certx && own0, Xc.x);
-            cert(oka && certx && own1, Xc.y);
-            cert(oka && owe, r1v);
+            rmax(mX, oka, own0, a0);
+            rmax(mX, oka, own1, a1);
+            if constexpr (APX) {
+                if constexpr (!ZB) {
+                    // X's values when certx (an inf times 0 is a NaN, dropped)
+                    M = rb2_vmax(M, rb2_max_abs2(Xc.x, Xc.y) * cxf);
+                } else {
+                    cert(oka && certx && own0, Xc.x);
+                    cert(oka && certx && own1, Xc.y);
+                }
+            }
+            certv(oka, owe, r1v);
             pin();
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -395,7 +450,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             const double v = rb2_sorc<APX>(rc, cf.slow, comp(Xm, e), sx, r1up + r1dn, r1v + r1m,
                                           comp(br[B0], e));
             y1v = (pin0 && ine) ? v : comp(Xm, e);
-            cert(ok0 && owe, y1v);
+            certv(ok0, owe, y1v);
             pin();
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -403,8 +458,8 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         double r2v;
         {
             const double cen = r1m;  // Y1' first-colour cell at q-1
-            const double zm = (qc == 1) ? cen : y1mm;
-            const double zp = (qc == nzi) ? cen : y1v;
+            const double zm = zc1 ? cen : y1mm;
+            const double zp = zcn ? cen : y1v;
             ydn = fdn ? cen : ydn;
             yup = fup ? cen : yup;
             double lf, rt;
@@ -424,8 +479,8 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             // update's sums; cell 1-e (second colour, value ob) reads the
             // first-colour cells of Y1' = R1 at q-1
             const double cb = ob;
-            const double wm = (qc == 1) ? cb : wm1;
-            const double wp = (qc == nzi) ? cb : r1c;
+            const double wm = zc1 ? cb : wm1;
+            const double wp = zcn ? cb : r1c;
             qdn = fdn ? cb : qdn;
             qup = fup ? cb : qup;
             double lf2, rt2;
@@ -444,9 +499,9 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 ae = res1(rc, DivC{}, cen, lf, rt, ydn, yup, zm, zp, comp(bm, e));
                 ab = res1(rc, DivC{}, cb, lf2, rt2, qdn, qup, wm, wp, comp(bm, 1 - e));
             }
-            mY = umax(okc && owe, ae, mY);
-            mY = umax(okc && owb, ab, mY);
-            cert(okc && owe, r2v);
+            rmax(mY, okc, owe, ae);
+            rmax(mY, okc, owb, ab);
+            certv(okc, owe, r2v);
             pin();
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -454,8 +509,8 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         double2 out;
         {
             const double cen = y1mm;  // Y1' second-colour cell at q-2
-            const double zm = (qd == 1) ? cen : zm2;
-            const double zp = (qd == nzi) ? cen : r2v;
+            const double zm = zd1 ? cen : zm2;
+            const double zp = zdn ? cen : r2v;
             wdn = fdn ? cen : wdn;
             wup = fup ? cen : wup;
             double lf, rt;
@@ -468,7 +523,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             }
             const double v = rb2_sorc<APX>(rc, cf.slow, cen, rt + lf, wup + wdn, zp + zm, bq2);
             const double y2v = (pind && ine) ? v : cen;
-            cert(okd && owe, y2v);
+            certv(okd, owe, y2v);
             pin();
             out = (e == 0) ? make_double2(y2v, ow) : make_double2(ow, y2v);
         }
@@ -495,31 +550,44 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 };
                 double* yq = Y + (long long)qd * g.ps;
                 put(yq);
-                if (qd == 1) put(yq - g.ps);
-                if (qd == nzi) put(yq + g.ps);
+                if (zd1) put(yq - g.ps);
+                if (zdn) put(yq + g.ps);
             }
         }
     };
     // E(q) = ((j + q + kofs) & 1) == 0, wave-uniform (rows r and r + 16 share it)
     const bool E0 = __builtin_amdgcn_readfirstlane(((j + q0 + g.kofs) & 1) == 0 ? 1 : 0) != 0;
     const int nsteps = ke - kb + 6;  // q0 .. ke + 1
+    // the steady steps: q in [max(kb + 2, 4), ke - 2] (every stage's plane in
+    // [kb, ke), none a z face or next to one, every operand from a plane the
+    // march wrote), entered at a multiple of 4 steps to keep the ring phases
+    const int n_s = min((max(kb + 2, 4) - q0 + 3) & ~3, nsteps);
+    const int n_e = ke - 2 - q0 + 1;
     int n = 0;
     auto march = [&](auto E0c) __attribute__((always_inline)) {
         constexpr bool A = decltype(E0c)::value;
         using TA = BoolC<A>;
         using TB = BoolC<!A>;
-        for (; n + 3 < nsteps; n += 4) {
-            step(TA{}, IntC<0>{}, q0 + n);
-            step(TB{}, IntC<1>{}, q0 + n + 1);
-            step(TA{}, IntC<2>{}, q0 + n + 2);
-            step(TB{}, IntC<3>{}, q0 + n + 3);
-        }
-        if (n < nsteps) step(TA{}, IntC<0>{}, q0 + n);
-        if (n + 1 < nsteps) step(TB{}, IntC<1>{}, q0 + n + 1);
-        if (n + 2 < nsteps) step(TA{}, IntC<2>{}, q0 + n + 2);
+        auto four = [&](auto Zc) __attribute__((always_inline)) {
+            step(TA{}, IntC<0>{}, Zc, q0 + n);
+            step(TB{}, IntC<1>{}, Zc, q0 + n + 1);
+            step(TA{}, IntC<2>{}, Zc, q0 + n + 2);
+            step(TB{}, IntC<3>{}, Zc, q0 + n + 3);
+        };
+        for (; n + 3 < n_s; n += 4) four(BoolC<true>{});
+        for (; n + 3 < n_e; n += 4) four(BoolC<false>{});
+        for (; n + 3 < nsteps; n += 4) four(BoolC<true>{});
+        if (n < nsteps) step(TA{}, IntC<0>{}, BoolC<true>{}, q0 + n);
+        if (n + 1 < nsteps) step(TB{}, IntC<1>{}, BoolC<true>{}, q0 + n + 1);
+        if (n + 2 < nsteps) step(TA{}, IntC<2>{}, BoolC<true>{}, q0 + n + 2);
     };
     if (E0) march(BoolC<true>{});
     else march(BoolC<false>{});
+    // the steady steps of an interior tile took every lane's residuals
+    if constexpr (!BND) {
+        mX = own ? mX : 0.0;
+        mY = own ? mY : 0.0;
+    }
 }
 
 template <bool APX, int FL>
@@ -555,25 +623,19 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
     const bool bnd = !(ilo >= 1 && ilo + 2 * RB2_TC - 1 <= g.nx - 3 && jlo >= 2 &&
                        jlo + RB2_TR - 1 <= g.ny - 3);
     double mX = 0.0, mY = 0.0, M = 0.0;
-    int emin = 0;
     if (bnd)
-        rb2_march<APX, FL, true>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M, emin);
+        rb2_march<APX, FL, true>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M);
     else
-        rb2_march<APX, FL, false>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M,
-                                  emin);
-    // ---- the sweep's maxima: partials[4 b + 0..3]; the last workgroup decides ----
+        rb2_march<APX, FL, false>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M);
+    // ---- the sweep's maxima: partials[4 b + 0..2]; the last workgroup decides ----
     mX = wave_max(mX);
     mY = wave_max(mY);
-    if constexpr (APX) {
-        M = wave_max(M);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) emin = min(emin, __shfl_down(emin, off, 64));
-    }
+    if constexpr (APX) M = wave_max(M);
     if (lane == 0) {
         L.sh[0][w] = mX;
         L.sh[1][w] = mY;
         L.sh[2][w] = M;
-        L.sh[3][w] = (double)emin;
+        L.sh[3][w] = 0.0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
