@@ -1,0 +1,243 @@
+// ccf.hpp -- one z-march per Chronopoulos-Gear CG iteration (k_ccf): one
+// device, 3-D, cg_variant 1 (the single-reduction CG of kernels.hpp k_cc1 /
+// k_cc2).
+//
+// Iteration it, from r_it (buffer R0), p_{it-1}, alpha_it and beta_it:
+//   p_it     = r_it + beta_it p_{it-1}              (FIRST: p_0 = r_0)
+//   s_it     = A p_it                               (the stencil, not the
+//                                                    recurrence w + beta s)
+//   r_{it+1} = r_it - alpha_it s_it                 (into buffer R1)
+//   w_{it+1} = A r_{it+1};  gamma = (r, r), delta = (w, r) at it + 1
+// and every CG_XFOLD-th iteration x += the four pending alpha_j p_j, in
+// k_cc1's order. Only r, p (and x on fold iterations) touch HBM: read r_it
+// and p_{it-1}, write p_it and r_{it+1}, 32 B per cell (k_cc1 + k_cc2: 72),
+// plus the fold's 40 B every fourth iteration. s and w are formed in
+// registers from p and r one and two cells out, so a tile carries a two-cell
+// halo and computes s and w on the fly instead of storing and re-reading
+// them; A = -lap7 with zero walls, as k_cc2.
+//
+// The iterates equal k_cc1 / k_cc2's up to rounding (s is A p_it itself, not
+// its recurrence; the dot products are summed per tile), which is what the
+// single-reduction tests gate against textbook CG (iterations +-2).
+//
+// Pipeline. Step q of the z march, per lane (an x pair of one row):
+//   a: p_it at plane q + 2 from the loaded r_it, p_{it-1}  (published in LDS)
+//   b: s_it and r_{it+1} at plane q + 1: in-plane p from LDS, z from the
+//      lane's ring; p_it and r_{it+1} stored there (published in LDS)
+//   c: w_{it+1} at plane q and the two dot products
+// one barrier per step; LDS holds p_it and r_{it+1} planes by parity.
+//
+// Tiles: 32 x pairs (64 columns) x 32 rows, 1024 threads, lane l of wave w
+// owns pair l % 32 of rows w and w + 16; 60 x 28 cells written per tile.
+#pragma once
+
+#include "kernels.hpp"
+
+namespace cfdhip {
+
+constexpr int CCF_TC = 32;  // x pairs per tile row
+constexpr int CCF_TR = 32;  // tile rows
+constexpr int CCF_OX = 60;  // columns written per tile
+constexpr int CCF_OY = 28;  // rows written per tile
+// LDS plane: rows of 2 padded halves (.x cells, then .y cells) so that an x
+// neighbour (one double of the adjacent lane) is a conflict-free 8-B read
+constexpr int CCF_LP = CCF_TC + 2;
+constexpr int CCF_LR = 2 * CCF_LP;
+constexpr int CCF_LS = (CCF_TR + 2) * CCF_LR;
+struct CcfLds {
+    double pl[4][CCF_LS];  // 0-1: p_it by plane parity, 2-3: r_{it+1} by parity
+    double sh[32];
+    int flag;
+};
+
+template <bool FIRST, bool FOLD>
+static __global__ __launch_bounds__(1024, 4) void k_ccf(
+    SGeo g, Lap Lp, const double* __restrict__ R0, double* __restrict__ R1,
+    const double* __restrict__ Po, double* __restrict__ Pn, PPrev pv, double* __restrict__ x,
+    CgState* st, double* partials, unsigned* counter, int it, int xmap) {
+    __shared__ CcfLds L;
+    if (st->done) return;
+    const double a = st->alpha[it % CG_XFOLD];
+    const double ma = -a;
+    const double beta = FIRST ? 0.0 : st->beta;
+    double aq[CG_XFOLD - 1];
+#pragma unroll
+    for (int q = 0; q < CG_XFOLD - 1; ++q)
+        aq[q] = FOLD ? st->alpha[(it + 1 + q) % CG_XFOLD] : 0.0;  // alpha_{it-3+q}
+    const int t = xmap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int tx = t % g.tiles_x;
+    const int rest = t / g.tiles_x;
+    const int ty = rest % g.tiles_y;
+    const int tz = rest / g.tiles_y;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int c = lane & 31;
+    const int r = w + 16 * (lane >> 5);
+    const int i0 = tx * CCF_OX - 2 + 2 * c;  // even; the pair is (i0, i0 + 1)
+    const int j = ty * CCF_OY - 2 + r;
+    const int kb = g.k0 + tz * g.kc;
+    const int ke = min(kb + g.kc, g.k1);
+    const bool jin = j >= 1 && j <= g.ny - 2;
+    const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;
+    const bool in1 = jin && i0 + 1 >= 1 && i0 + 1 <= g.nx - 2;
+    // written / reduced: pairs 1..30 of rows 2..29 that hold a grid pair
+    const bool own = c >= 1 && c <= CCF_TC - 2 && r >= 2 && r <= CCF_TR - 3;
+    const bool wr = own && jin && i0 >= 0 && i0 < g.nx;
+    // loads from always-valid addresses: outside the grid they hold other
+    // cells' values, which only feed cells outside the interior (masked)
+    const int ic = i0 < 0 ? 0 : (i0 < g.nx ? i0 : g.nx - 2 - ((g.nx - 2) & 1));
+    const int col = max(min(j, g.ny - 1), 0) * (int)g.px + ic;
+    auto plane = [&](int k) -> long long { return (long long)min(max(k, 0), g.nz - 1) * g.ps; };
+    // LDS: one base at the lane's cell minus one row and one column of the
+    // padded plane, so every operand is a non-negative immediate offset
+    double* const Lb = &L.pl[0][r * CCF_LR + c];
+    constexpr int OWX = CCF_LR + 1, OWY = CCF_LR + 1 + CCF_LP;
+    constexpr int LFo = CCF_LR + CCF_LP, RTo = CCF_LR + 2;  // pair c-1 .y, pair c+1 .x
+    constexpr int DNX = 1, DNY = 1 + CCF_LP, UPX = 2 * CCF_LR + 1, UPY = 2 * CCF_LR + 1 + CCF_LP;
+    auto lrd = [&](int pl, int d) __attribute__((always_inline)) -> double {
+        // keeps each read a ds_read_b64 (see rb2.hpp)
+        __builtin_amdgcn_sched_barrier(0x7ff);
+        return Lb[pl * CCF_LS + d];
+    };
+    auto lput = [&](int pl, double2 v) __attribute__((always_inline)) {
+        Lb[pl * CCF_LS + OWX] = v.x;
+        Lb[pl * CCF_LS + OWY] = v.y;
+    };
+    // zero the pads (never written; halo lanes read them)
+    for (int e = threadIdx.x; e < 4 * CCF_LS; e += 1024) {
+        const int q = e % CCF_LS;
+        const int row = q / CCF_LR, cc = q % CCF_LP;
+        if (row == 0 || row == CCF_TR + 1 || cc == 0 || cc == CCF_LP - 1) L.pl[e / CCF_LS][q] = 0.0;
+    }
+    // -A v at the pair from its own pair (v), its z neighbours and the plane's LDS
+    auto stencil = [&](int pl, double2 v, double2 zm, double2 zp, double2& out)
+                       __attribute__((always_inline)) {
+        const double lf = lrd(pl, LFo), rt = lrd(pl, RTo);
+        const double dx = lrd(pl, DNX), dy = lrd(pl, DNY);
+        const double ux = lrd(pl, UPX), uy = lrd(pl, UPY);
+        out.x = -lap7(Lp, v.x, lf, v.y, dx, ux, zm.x, zp.x);
+        out.y = -lap7(Lp, v.y, v.x, rt, dy, uy, zm.y, zp.y);
+    };
+    const int q0 = kb - 4;  // steps q0 .. ke - 1 (see the header)
+    const int nsteps = ke - kb + 4;
+    // rings (slot of plane p at step q: (p - q0) & 3): r_it, p_{it-1} (loaded
+    // two steps ahead), p_it, r_{it+1}; fold operands (x, p_{it-3..it-1}) by parity
+    double2 rr[4], po[4], pn[4], rn[4];
+    double2 fx[2], f0[2], f1[2], f2[2];
+    const double2 zero = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) pn[s] = rn[s] = po[s] = rr[s] = zero;
+    rr[1] = ld2(R0, plane(q0 + 1) + col);
+    rr[2] = ld2(R0, plane(q0 + 2) + col);
+    rr[3] = ld2(R0, plane(q0 + 3) + col);
+    if (!FIRST) {
+        po[2] = ld2(Po, plane(q0 + 2) + col);
+        po[3] = ld2(Po, plane(q0 + 3) + col);
+    }
+    if (FOLD) {
+        const long long o = plane(q0 + 1) + col;
+        fx[1] = ld2(x, o);
+        f0[1] = ld2(pv.q[0], o);
+        f1[1] = ld2(pv.q[1], o);
+        f2[1] = ld2(pv.q[2], o);
+    }
+    double accg = 0.0, accd = 0.0;
+    auto step = [&](auto Pc, int q) __attribute__((always_inline)) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
+        constexpr int SM = (P + 3) & 3;  // plane q - 1 (r_{it+1})
+        constexpr int F1 = (P + 1) & 1, F2 = P & 1;  // fold slots of planes q + 1, q + 2
+        constexpr int LPR = (P + 1) & 1, LPW = P & 1;        // p_it planes q + 1 (read), q + 2
+        constexpr int LRR = 2 + (P & 1), LRW = 2 + ((P + 1) & 1);  // r_{it+1} q (read), q + 1
+        // prefetch plane q + 4 (r_it, p_{it-1}: two steps, 64 KB per CU in
+        // flight; one step's 32 KB held a CU to ~17 GB/s) and the fold
+        // operands of q + 2
+        rr[S0] = ld2(R0, plane(q + 4) + col);
+        if (!FIRST) po[S0] = ld2(Po, plane(q + 4) + col);
+        if (FOLD) {
+            const long long o = plane(q + 2) + col;
+            fx[F2] = ld2(x, o);
+            f0[F2] = ld2(pv.q[0], o);
+            f1[F2] = ld2(pv.q[1], o);
+            f2[F2] = ld2(pv.q[2], o);
+        }
+        __syncthreads();
+        // ---- a: p_it at q + 2 ----
+        const double2 p2 = FIRST ? rr[S2] : fma2p(rr[S2], beta, po[S2]);
+        pn[S2] = p2;
+        // ---- b: s_it, r_{it+1} at q + 1 ----
+        double2 s;
+        stencil(LPR, pn[S1], pn[S0], p2, s);
+        const int qb = q + 1;
+        const bool kbin = qb >= 1 && qb <= g.nz - 2;
+        const double2 rv = rr[S1];
+        const double2 r1 = make_double2((kbin && in0) ? rv.x + ma * s.x : 0.0,
+                                        (kbin && in1) ? rv.y + ma * s.y : 0.0);
+        rn[S1] = r1;
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- c: w_{it+1} at q, the dot products ----
+        double2 wv;
+        stencil(LRR, rn[S0], rn[SM], r1, wv);
+        if (q >= kb && own) {
+            const double2 rc = rn[S0];
+            if (in0) {
+                accg += rc.x * rc.x;
+                accd += wv.x * rc.x;
+            }
+            if (in1) {
+                accg += rc.y * rc.y;
+                accd += wv.y * rc.y;
+            }
+        }
+        // ---- publish p_it (q + 2), r_{it+1} (q + 1); stores at q + 1 ----
+        lput(LPW, p2);
+        lput(LRW, r1);
+        {
+            const int bo = (qb >= kb && qb < ke && wr) ? col * 8 : ST_NOSTORE;
+            const long long pb = plane(qb);
+            const double2 p1 = pn[S1];
+            st2b<false>(Pn + pb, g.ps, bo, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
+            st2b<false>(R1 + pb, g.ps, bo, r1);
+            if (FOLD) {
+                const double2 xo = fx[F1], qa = f0[F1], qq = f1[F1], qc = f2[F1];
+                double2 xw;
+                xw.x = in0 ? (((xo.x + aq[0] * qa.x) + aq[1] * qq.x) + aq[2] * qc.x) + a * p1.x
+                           : xo.x;
+                xw.y = in1 ? (((xo.y + aq[0] * qa.y) + aq[1] * qq.y) + aq[2] * qc.y) + a * p1.y
+                           : xo.y;
+                st2b<false>(x + pb, g.ps, bo, xw);
+            }
+        }
+    };
+    int n = 0;
+    for (; n + 3 < nsteps; n += 4) {
+        step(IntC<0>{}, q0 + n);
+        step(IntC<1>{}, q0 + n + 1);
+        step(IntC<2>{}, q0 + n + 2);
+        step(IntC<3>{}, q0 + n + 3);
+    }
+    if (n < nsteps) step(IntC<0>{}, q0 + n);
+    if (n + 1 < nsteps) step(IntC<1>{}, q0 + n + 1);
+    if (n + 2 < nsteps) step(IntC<2>{}, q0 + n + 2);
+    // ---- one reduction: (gamma, delta) of iteration it + 1 ----
+    accg = wave_sum(accg);
+    accd = wave_sum(accd);
+    __syncthreads();
+    if (lane == 0) {
+        L.sh[w] = accg;
+        L.sh[16 + w] = accd;
+    }
+    __syncthreads();
+    double bg = 0.0, bd = 0.0;
+    if (threadIdx.x == 0)
+        for (int v = 0; v < 16; ++v) {
+            bg += L.sh[v];
+            bd += L.sh[16 + v];
+        }
+    double tg, td;
+    double* shs = &L.pl[0][0];
+    if (grid_sum2_last<1024>(bg, bd, partials, counter, shs, &L.flag, tg, td) && threadIdx.x == 0)
+        fin_cc(st, tg, td, it, FOLD);
+}
+
+}  // namespace cfdhip

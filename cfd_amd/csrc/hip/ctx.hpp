@@ -133,6 +133,8 @@ struct hip_proj_ctx {
     RxState* rxst = nullptr;             // fused relaxation loop state
     RxState* rxst2 = nullptr;            // scratch state of k_rb2's recompute sweeps
     SGeo r2geo{};                        // two-iterations-per-sweep RB-SOR tiling (k_rb2)
+    SGeo ccgeo{};                        // fused single-reduction CG tiling (k_ccf)
+    double* r2 = nullptr;                // k_ccf: r_{it+1} when r_it is in r (by parity)
     double* partials = nullptr;
     unsigned* counter = nullptr;
     unsigned long long* red = nullptr;   // [0] max |u|^2, [1] max |p|, [2] nonfinite, [3] max T, [4] residual

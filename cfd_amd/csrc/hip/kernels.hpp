@@ -443,6 +443,25 @@ __device__ __forceinline__ void st2v(double* p, long long i, double2 v) {
         *reinterpret_cast<double2*>(p + i) = v;
     }
 }
+// A 16-B store into one plane through a buffer resource: an offset past the
+// plane's bytes is dropped by the hardware, so a lane (or a step) that must
+// not store passes ST_NOSTORE instead of branching around the store. Every
+// step of a march then issues the same stores, and the compiler's vmcnt
+// counting stays exact (a store under a branch counts as possibly absent, so
+// the wait for a later plane's loads would also wait for that store).
+constexpr int ST_NOSTORE = 0x7ffffff0;
+template <bool NT>
+__device__ __forceinline__ void st2b(double* plane_base, long long plane_elems, int boff,
+                                     double2 v) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(plane_base, 0, (int)(plane_elems * 8), 0x00020000);
+    const unsigned long long bx = (unsigned long long)__double_as_longlong(v.x);
+    const unsigned long long by = (unsigned long long)__double_as_longlong(v.y);
+    const u4 d = {(unsigned)bx, (unsigned)(bx >> 32), (unsigned)by, (unsigned)(by >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, rs, boff, 0, NT ? 2 : 0);  // aux 2: nt
+}
+
 template <int FL>
 __device__ __forceinline__ double2 ld2v(const double* p, long long i) {
     if (FL & SW_NT_LOAD) {
@@ -499,6 +518,9 @@ constexpr int SW_PREFETCH = 4;
 // neighbouring tile re-reads as its y halo) are loaded non-temporally.
 constexpr int SW_EDGE1 = 8;
 constexpr int SW_NT_INNER = 16;
+// bit 5: the plane's store through a buffer resource with an out-of-range
+// offset for the lanes that do not store (st2b), instead of a branch
+constexpr int SW_BUFST = 32;
 // (r01e: asking for 8 waves per SIMD, i.e. <= 64 VGPRs and two 1024-thread
 // workgroups per CU, spills and is slower; profiles/r01e_sweep_variants.jsonl)
 template <int FL>
@@ -553,6 +575,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     const double* __restrict__ fq2 = fd.q2;
     double* __restrict__ fx = fd.x;
     RowPair c = row_pair<TY>(g);
+    const int colp = (int)(c.idx - (long long)c.kb * g.ps);  // in-plane offset (SW_BUFST)
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
     const int hslot = (c.w == 0) ? 0 : TY + 1;
@@ -645,7 +668,17 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
         if (c.lane == 63) right = E1 ? form1(cur.lr, cur.lo) : form1(cur.rr, cur.ro);
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
-        if (FOLD && c.act) {
+        if constexpr ((FL & SW_BUFST) != 0 && FOLD) {
+            double2 xw;
+            xw.x = c.in0 ? (((cur.fxo.x + fa[0] * cur.f4.x) + fa[1] * cur.f3.x) + fa[2] * cur.f2.x) +
+                               fa[3] * praw.x
+                         : cur.fxo.x;
+            xw.y = c.in1 ? (((cur.fxo.y + fa[0] * cur.f4.y) + fa[1] * cur.f3.y) + fa[2] * cur.f2.y) +
+                               fa[3] * praw.y
+                         : cur.fxo.y;
+            st2b<(FL & SW_NT_STORE) != 0>(fx + (long long)k * g.ps, g.ps,
+                                          c.act ? colp * 8 : ST_NOSTORE, xw);
+        } else if (FOLD && c.act) {
             double2 xw;
             xw.x = c.in0 ? (((cur.fxo.x + fa[0] * cur.f4.x) + fa[1] * cur.f3.x) + fa[2] * cur.f2.x) +
                                fa[3] * praw.x
@@ -655,7 +688,11 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
                          : cur.fxo.y;
             st2v<FL>(fx, idx, xw);
         }
-        if (c.act) {
+        if constexpr ((FL & SW_BUFST) != 0) {
+            const double2 pw = make_double2(c.in0 ? pc.x : 0.0, c.in1 ? pc.y : 0.0);
+            st2b<(FL & SW_NT_STORE) != 0>(pn + (long long)k * g.ps, g.ps,
+                                          c.act ? colp * 8 : ST_NOSTORE, pw);
+        } else if (c.act) {
             double2 pw;
             pw.x = c.in0 ? pc.x : 0.0;
             pw.y = c.in1 ? pc.y : 0.0;
@@ -725,6 +762,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     if (st->done) return;
     const double malpha = -st->alpha[it % CG_XFOLD];
     RowPair c = row_pair<TY>(g);
+    const int colp = (int)(c.idx - (long long)c.kb * g.ps);  // in-plane offset (SW_BUFST)
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
     const int hslot = (c.w == 0) ? 0 : TY + 1;
@@ -797,7 +835,11 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         double2 rn;
         rn.x = c.in0 ? cur.rr.x + malpha * Ap0 : cur.rr.x;
         rn.y = c.in1 ? cur.rr.y + malpha * Ap1 : cur.rr.y;
-        if (c.act) st2v<FL>(r, idx, rn);
+        if constexpr ((FL & SW_BUFST) != 0)
+            st2b<(FL & SW_NT_STORE) != 0>(r + (long long)k * g.ps, g.ps,
+                                          c.act ? colp * 8 : ST_NOSTORE, rn);
+        else if (c.act)
+            st2v<FL>(r, idx, rn);
         if (c.in0) acc += rn.x * rn.x;
         if (c.in1) acc += rn.y * rn.y;
         pm = pc;
@@ -2372,8 +2414,16 @@ __device__ __forceinline__ void rb1_body(
     auto& rb = *reinterpret_cast<double(*)[2][TR][2][TC]>(L.rb);
     auto& sh = L.sh;
     auto& flag = L.flag;
+    // every LDS read stays a ds_read_b64 (2 LDS cycles per wave; a pair
+    // merged into ds_read2_b64 takes 8): a scheduling barrier that lets every
+    // instruction class cross it ends the pairing pass's search window
+    auto lrd = [&](const double& v) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0x7ff);
+        return v;
+    };
     auto lget = [&](double (&a)[2][TR][2][TC], int p, int r, int l) __attribute__((always_inline)) {
-        return make_double2(a[p][r][0][l], a[p][r][1][l]);
+        const double x = lrd(a[p][r][0][l]);
+        return make_double2(x, lrd(a[p][r][1][l]));
     };
     auto lput = [&](double (&a)[2][TR][2][TC], int p, int r, int l, double2 v)
                     __attribute__((always_inline)) {
@@ -2508,7 +2558,7 @@ __device__ __forceinline__ void rb1_body(
         // round trip after the barrier serves both halves of the step
         const double2 rys = lget(rb, q & 1, rlo, c);
         const double2 ryn = lget(rb, q & 1, rhi, c);
-        const double rlr = E ? rb[q & 1][r][1][cm] : rb[q & 1][r][0][cp];
+        const double rlr = lrd(E ? rb[q & 1][r][1][cm] : rb[q & 1][r][0][cp]);
         double2 R = xc;
         if constexpr (DIST) {
             if ((qa == g.k0 - 1 && rh_lo) || (qa == g.k1 && rh_hi))
@@ -2516,8 +2566,8 @@ __device__ __forceinline__ void rb1_body(
         }
         const double2 ys = lget(xb, qa & 1, rlo, c);
         const double2 yn = lget(xb, qa & 1, rhi, c);
-        const double left = xb[qa & 1][r][1][cm];
-        const double right = xb[qa & 1][r][0][cp];
+        const double left = lrd(xb[qa & 1][r][1][cm]);
+        const double right = lrd(xb[qa & 1][r][0][cp]);
         if (wr && qin) {
             if (E) {
                 const double v = sor1(rc, DivC{}, xc.x, left, xc.y, ys.x, yn.x, xm.x, xp.x, bq.x);

@@ -11,6 +11,7 @@
 // iteration, poisson_cg_gpu_solve.cuh:189-203).
 #include "ctx.hpp"
 #include "rb2.hpp"
+#include "ccf.hpp"
 
 template <int TY, bool FIRST, bool DIST, int FL, bool FOLD>
 static void launch_cgA_t(hip_proj_ctx* c, const Lap& L, const double* r, const double* po,
@@ -76,6 +77,7 @@ static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double
         case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it, fd);
         case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it, fd);
         case 15: return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it, fd);
+        case 47: return launch_cgA_f<TY, 47>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
         case 23: if constexpr (TY == 16) return launch_cgA_f<TY, 23>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
@@ -94,6 +96,7 @@ static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BA
         case 4: return launch_cgB_f<TY, 4>(c, sg, L, a, it);
         case 7: return launch_cgB_f<TY, 7>(c, sg, L, a, it);
         case 15: return launch_cgB_f<TY, 15>(c, sg, L, a, it);
+        case 47: return launch_cgB_f<TY, 47>(c, sg, L, a, it);
                  [[fallthrough]];
         case 23: if constexpr (TY == 16) return launch_cgB_f<TY, 23>(c, sg, L, a, it);
                  [[fallthrough]];
@@ -155,6 +158,28 @@ static void launch_cc2(hip_proj_ctx* c, const Lap& L, int it, bool init) {
     return launch_cc2_ty<8>(c, L, it, init);
 }
 
+// k_ccf (ccf.hpp): cg_variant 1's whole iteration in one z-march; r_it is in
+// c->r for even it and in c->r2 for odd it
+template <bool FIRST, bool FOLD>
+static void launch_ccf_t(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
+                         const PPrev& pv, double* x, int it, int xmap) {
+    const SGeo& g = c->ccgeo;
+    const double* r0 = (it & 1) ? c->r2 : c->r;
+    double* r1 = (it & 1) ? c->r : c->r2;
+    hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
+                          dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, r0, r1, po, pn, pv, x,
+                          c->st, c->partials, c->counter, it, xmap);
+}
+
+static void launch_ccf(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
+                       const PPrev& pv, double* x, int it) {
+    static const int xmap = getenv("CFD_HIP_CCF_XMAP") ? atoi(getenv("CFD_HIP_CCF_XMAP")) : 0;
+    const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
+    if (it == 0) launch_ccf_t<true, false>(c, L, pn, po, pv, x, it, xmap);
+    else if (fold) launch_ccf_t<false, true>(c, L, pn, po, pv, x, it, xmap);
+    else launch_ccf_t<false, false>(c, L, pn, po, pv, x, it, xmap);
+}
+
 // ---------------------------------------------------------------------------
 // pressure solvers on ctx->pn
 // ---------------------------------------------------------------------------
@@ -169,8 +194,8 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     const bool D = dist(c);
     double* x = c->pn;
     if (c->cg_scratch_dirty) {  // after RK4 stages (rk4_hip.hip): walls of r / p ring to 0
-        for (double* f : {c->r, c->pa, c->pb, c->pc4, c->pd4})
-            HIP_TRY(hipMemsetAsync(f, 0, field_elems(c) * sizeof(double), c->stream));
+        for (double* f : {c->r, c->pa, c->pb, c->pc4, c->pd4, c->r2})
+            if (f) HIP_TRY(hipMemsetAsync(f, 0, field_elems(c) * sizeof(double), c->stream));
         c->cg_scratch_dirty = 0;
     }
     ST_TRY(halo(c, {x}));
@@ -263,6 +288,10 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     // Chronopoulos-Gear (cg_variant 1): k_cc1 (pointwise) -> halo of r ->
     // k_cc2 (w = A r and both dots, ONE reduction / all-reduce)
     const bool cc = (c->cfg.cg_variant == 1);
+    // one device, 3-D: the fused iteration (k_ccf); CFD_HIP_CCF = 0 keeps
+    // k_cc1 + k_cc2 (read per solve: tests switch it)
+    const char* eccf = getenv("CFD_HIP_CCF");
+    const bool ccf = cc && !D && c->ccgeo.tiles_x > 0 && !(eccf && atoi(eccf) == 0);
     auto reduce_cc = [&](int it, bool init) -> cfd_status_t {
         if (!D || mbox(c)) return CFD_SUCCESS;
         return timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
@@ -277,6 +306,10 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         double* pold = P[(it + CG_XFOLD - 1) % CG_XFOLD];
         PPrev pv;
         for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];
+        if (ccf) {
+            timed(c, HIP_KT_CC_FUSED, [&] { launch_ccf(c, L, pnew, pold, pv, x, it); }, it);
+            return CFD_SUCCESS;
+        }
         timed(c, HIP_KT_CC_UPDATE, [&] { launch_cc1(c, pnew, pold, pv, x, it); }, it);
         if (D)
             ST_TRY(timed_span(c, c->stream, HIP_KT_HALO,
@@ -287,7 +320,8 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     if (cc) {
         const size_t n = field_elems(c);
         if (!c->cw) ST_TRY(dalloc(c, &c->cw, n));
-        if (!c->cs) ST_TRY(dalloc(c, &c->cs, n));
+        if (!ccf && !c->cs) ST_TRY(dalloc(c, &c->cs, n));
+        if (ccf && !c->r2) ST_TRY(dalloc(c, &c->r2, n));
         // w_0 = A r_0 and alpha_0 (the textbook's first (p, Ap) with p_0 = r_0)
         timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, -1, true); });
         ST_TRY(reduce_cc(-1, true));
@@ -1124,9 +1158,13 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
     {   // variants built: 0-3 (memory hints), 4 and 7 (+ plane prefetch)
         const int v = c->cfg.sweep_variant & 63;
-        if (v == 15 && c->sweep_ty >= 8) c->sweep_variant = v;
+        if ((v == 15 || v == 47) && c->sweep_ty >= 8) c->sweep_variant = v;
         else if ((v == 23 || v == 31) && c->sweep_ty == 16) c->sweep_variant = v;
         else c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : (v & 3);
+        // experiments: CFD_HIP_SWEEP_BUFST=1 stores through st2b (variant 47)
+        if (c->sweep_variant == 15 && getenv("CFD_HIP_SWEEP_BUFST") &&
+            atoi(getenv("CFD_HIP_SWEEP_BUFST")) == 1)
+            c->sweep_variant = 47;
     }
     {
         const int vf = c->cfg.sweep_variant_fold;
@@ -1218,6 +1256,24 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             r2.kc = std::max(1, std::min(r2.kc, nint_k));
             r2.tiles_z = (nint_k + r2.kc - 1) / r2.kc;
             n_partials = std::max(n_partials, 2 * r2.tiles_x * r2.tiles_y * r2.tiles_z);
+        }
+        // the fused single-reduction CG iteration (k_ccf, ccf.hpp): 64 x 32
+        // cells loaded, 60 x 28 written; one device, 3-D
+        SGeo& cg = c->ccgeo;
+        cg = rg;
+        cg.tiles_x = cg.tiles_y = cg.tiles_z = 0;
+        if (c->nranks == 1 && nz >= 3 && nx >= 4 && ny >= 4) {
+            cg.xofs = 0;
+            cg.tiles_x = (int)((nx - 1 + CCF_OX - 1) / CCF_OX);
+            cg.tiles_y = (int)((ny - 1 + CCF_OY - 1) / CCF_OY);
+            cg.kc = 128;
+            if (const char* e = getenv("CFD_HIP_CCF_KC")) cg.kc = std::max(1, atoi(e));
+            while (cg.kc > 4 &&
+                   (long long)cg.tiles_x * cg.tiles_y * ((nint_k + cg.kc - 1) / cg.kc) < 512)
+                cg.kc /= 2;
+            cg.kc = std::max(1, std::min(cg.kc, nint_k));
+            cg.tiles_z = (nint_k + cg.kc - 1) / cg.kc;
+            n_partials = std::max(n_partials, cg.tiles_x * cg.tiles_y * cg.tiles_z);
         }
         // the last x tile of a TC-64 launch is partial unless 124 divides the
         // row: its workgroups run a full tile's steps for a few columns

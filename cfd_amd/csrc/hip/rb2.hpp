@@ -534,7 +534,12 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         st(RB2_PR1 + A1n, r1v);
         st(RB2_PY1 + AYn, y1v);
         st(RB2_PR2 + A2n, r2v);
-        if (okd) {
+        if constexpr (!ZB && !BND) {
+            // steady step of an interior tile: one store, never branched
+            // around (st2b), so the loads' vmcnt waits exclude it
+            st2b<(FL & SW_NT_STORE) != 0>(Y + (long long)qd * g.ps, g.ps,
+                                          own ? col * 8 : ST_NOSTORE, out);
+        } else if (okd) {
             // the Neumann shell folded into the stores (as k_rb1)
             if (nrole & 1) out.x = out.y;
             if (nrole & 2) out.y = out.x;

@@ -149,7 +149,9 @@ typedef enum {
                               device-mailbox reduction runs inside the sweep instead */
     HIP_KT_CG_SMALL = 14,  /* small grids: the whole CG solve in one cooperative launch */
     HIP_KT_RELAX2 = 15,    /* RB-SOR: one sweep of TWO iterations (k_rb2, one device, 3-D) */
-    HIP_KT_COUNT = 16
+    HIP_KT_CC_FUSED = 16,  /* cg_variant 1: the whole iteration in one z-march (k_ccf, one
+                              device, 3-D) */
+    HIP_KT_COUNT = 17
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);
