@@ -49,6 +49,8 @@ BYTES_SWEEP_AX = 64.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2};
                         # (the 4 pending alpha p folded; p_{it-1} is sweep A's p_old)
 BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
 BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
+BYTES_CC_FUSED = 42.0   # cg_variant 1 on one device, k_ccf: read r, p_old; write p, r (32)
+                        # + the x fold's 40 B every 4th iteration (mean per iteration)
 BYTES_CG_SMALL_ITER = 64.0    # small grids, k_cg_small per iteration (x updated every iteration)
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
 BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
@@ -252,6 +254,8 @@ def main():
                               bpc_small * n_loc / (avg * 1e-3) / 1e9, small_ms)
     if small_n:  # one iteration = the solve's time / its iterations
         cg_iter_ms = small_ms / max(1, sum(iters))
+    elif args.cg_variant == 1 and "cc_fused" in sweeps:  # one launch per iteration
+        cg_iter_ms = sweeps["cc_fused"][2] or 0.0
     elif args.cg_variant == 1:  # one iteration = update + SpMV
         cg_iter_ms = (sweeps["cc_update"][2] or 0.0) + (sweeps["cc_spmv"][2] or 0.0)
     else:  # one CG iteration = the mean of the two sweep A forms + sweep B
@@ -602,6 +606,10 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
     d = "true" if dist_ else "false"
     # sweep B marches z downwards on one device (CFD_HIP_CGB_REV=0: upwards)
     rev = "true" if (not dist_ and os.environ.get("CFD_HIP_CGB_REV", "1") != "0") else "false"
+    if cg_variant == 1 and not dist_:
+        # one z-march per iteration (ccf.hpp); the timer spans the plain and
+        # the fold launches, so the byte count is their mean
+        return (("cc_fused", "k_ccf<false, false>", BYTES_CC_FUSED),)
     if cg_variant == 1:
         return (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
                 ("cc_spmv", f"k_cc2<{rows}, {d}, false>", BYTES_CC_SPMV))

@@ -121,7 +121,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     const int q0 = kb - 4;  // steps q0 .. ke - 1 (see the header)
     const int nsteps = ke - kb + 4;
     // rings (slot of plane p at step q: (p - q0) & 3): r_it, p_{it-1} (loaded
-    // two steps ahead), p_it, r_{it+1}; fold operands (x, p_{it-3..it-1}) by parity
+    // one step ahead), p_it, r_{it+1}; fold operands (x, p_{it-3..it-1}) by parity
     double2 rr[4], po[4], pn[4], rn[4];
     double2 fx[2], f0[2], f1[2], f2[2];
     const double2 zero = make_double2(0.0, 0.0);
@@ -129,11 +129,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     for (int s = 0; s < 4; ++s) pn[s] = rn[s] = po[s] = rr[s] = zero;
     rr[1] = ld2(R0, plane(q0 + 1) + col);
     rr[2] = ld2(R0, plane(q0 + 2) + col);
-    rr[3] = ld2(R0, plane(q0 + 3) + col);
-    if (!FIRST) {
-        po[2] = ld2(Po, plane(q0 + 2) + col);
-        po[3] = ld2(Po, plane(q0 + 3) + col);
-    }
+    if (!FIRST) po[2] = ld2(Po, plane(q0 + 2) + col);
     if (FOLD) {
         const long long o = plane(q0 + 1) + col;
         fx[1] = ld2(x, o);
@@ -149,11 +145,11 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         constexpr int F1 = (P + 1) & 1, F2 = P & 1;  // fold slots of planes q + 1, q + 2
         constexpr int LPR = (P + 1) & 1, LPW = P & 1;        // p_it planes q + 1 (read), q + 2
         constexpr int LRR = 2 + (P & 1), LRW = 2 + ((P + 1) & 1);  // r_{it+1} q (read), q + 1
-        // prefetch plane q + 4 (r_it, p_{it-1}: two steps, 64 KB per CU in
-        // flight; one step's 32 KB held a CU to ~17 GB/s) and the fold
-        // operands of q + 2
-        rr[S0] = ld2(R0, plane(q + 4) + col);
-        if (!FIRST) po[S0] = ld2(Po, plane(q + 4) + col);
+        // prefetch plane q + 3 (r_it, p_{it-1}) and the fold operands of q + 2
+        // (two steps ahead measured slower: 1.32 vs 1.27 ms per iteration at
+        // 512^3, profiles/r04_ccf_prefetch2_cg_variant.jsonl)
+        rr[S3] = ld2(R0, plane(q + 3) + col);
+        if (!FIRST) po[S3] = ld2(Po, plane(q + 3) + col);
         if (FOLD) {
             const long long o = plane(q + 2) + col;
             fx[F2] = ld2(x, o);

@@ -518,9 +518,6 @@ constexpr int SW_PREFETCH = 4;
 // neighbouring tile re-reads as its y halo) are loaded non-temporally.
 constexpr int SW_EDGE1 = 8;
 constexpr int SW_NT_INNER = 16;
-// bit 5: the plane's store through a buffer resource with an out-of-range
-// offset for the lanes that do not store (st2b), instead of a branch
-constexpr int SW_BUFST = 32;
 // (r01e: asking for 8 waves per SIMD, i.e. <= 64 VGPRs and two 1024-thread
 // workgroups per CU, spills and is slower; profiles/r01e_sweep_variants.jsonl)
 template <int FL>
@@ -575,7 +572,6 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
     const double* __restrict__ fq2 = fd.q2;
     double* __restrict__ fx = fd.x;
     RowPair c = row_pair<TY>(g);
-    const int colp = (int)(c.idx - (long long)c.kb * g.ps);  // in-plane offset (SW_BUFST)
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
     const int hslot = (c.w == 0) ? 0 : TY + 1;
@@ -668,17 +664,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
         if (c.lane == 63) right = E1 ? form1(cur.lr, cur.lo) : form1(cur.rr, cur.ro);
         const double Ap0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double Ap1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
-        if constexpr ((FL & SW_BUFST) != 0 && FOLD) {
-            double2 xw;
-            xw.x = c.in0 ? (((cur.fxo.x + fa[0] * cur.f4.x) + fa[1] * cur.f3.x) + fa[2] * cur.f2.x) +
-                               fa[3] * praw.x
-                         : cur.fxo.x;
-            xw.y = c.in1 ? (((cur.fxo.y + fa[0] * cur.f4.y) + fa[1] * cur.f3.y) + fa[2] * cur.f2.y) +
-                               fa[3] * praw.y
-                         : cur.fxo.y;
-            st2b<(FL & SW_NT_STORE) != 0>(fx + (long long)k * g.ps, g.ps,
-                                          c.act ? colp * 8 : ST_NOSTORE, xw);
-        } else if (FOLD && c.act) {
+        if (FOLD && c.act) {
             double2 xw;
             xw.x = c.in0 ? (((cur.fxo.x + fa[0] * cur.f4.x) + fa[1] * cur.f3.x) + fa[2] * cur.f2.x) +
                                fa[3] * praw.x
@@ -688,11 +674,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgA(
                          : cur.fxo.y;
             st2v<FL>(fx, idx, xw);
         }
-        if constexpr ((FL & SW_BUFST) != 0) {
-            const double2 pw = make_double2(c.in0 ? pc.x : 0.0, c.in1 ? pc.y : 0.0);
-            st2b<(FL & SW_NT_STORE) != 0>(pn + (long long)k * g.ps, g.ps,
-                                          c.act ? colp * 8 : ST_NOSTORE, pw);
-        } else if (c.act) {
+        if (c.act) {
             double2 pw;
             pw.x = c.in0 ? pc.x : 0.0;
             pw.y = c.in1 ? pc.y : 0.0;
@@ -762,7 +744,6 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
     if (st->done) return;
     const double malpha = -st->alpha[it % CG_XFOLD];
     RowPair c = row_pair<TY>(g);
-    const int colp = (int)(c.idx - (long long)c.kb * g.ps);  // in-plane offset (SW_BUFST)
     const bool halo = (c.w == 0) || (c.w == TY - 1);
     const int jh = (c.w == 0) ? max(c.j - 1, 0) : min(c.j + 1, g.ny - 1);
     const int hslot = (c.w == 0) ? 0 : TY + 1;
@@ -835,11 +816,7 @@ static __global__ __launch_bounds__(64 * TY, sweep_min_waves<FL>()) void k_cgB(
         double2 rn;
         rn.x = c.in0 ? cur.rr.x + malpha * Ap0 : cur.rr.x;
         rn.y = c.in1 ? cur.rr.y + malpha * Ap1 : cur.rr.y;
-        if constexpr ((FL & SW_BUFST) != 0)
-            st2b<(FL & SW_NT_STORE) != 0>(r + (long long)k * g.ps, g.ps,
-                                          c.act ? colp * 8 : ST_NOSTORE, rn);
-        else if (c.act)
-            st2v<FL>(r, idx, rn);
+        if (c.act) st2v<FL>(r, idx, rn);
         if (c.in0) acc += rn.x * rn.x;
         if (c.in1) acc += rn.y * rn.y;
         pm = pc;

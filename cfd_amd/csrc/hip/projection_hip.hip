@@ -77,7 +77,6 @@ static void launch_cgA_v(hip_proj_ctx* c, bool first, const Lap& L, const double
         case 4: return launch_cgA_f<TY, 4>(c, first, L, r, po, pn, it, fd);
         case 7: return launch_cgA_f<TY, 7>(c, first, L, r, po, pn, it, fd);
         case 15: return launch_cgA_f<TY, 15>(c, first, L, r, po, pn, it, fd);
-        case 47: return launch_cgA_f<TY, 47>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
         case 23: if constexpr (TY == 16) return launch_cgA_f<TY, 23>(c, first, L, r, po, pn, it, fd);
                  [[fallthrough]];
@@ -96,7 +95,6 @@ static void launch_cgB_v(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BA
         case 4: return launch_cgB_f<TY, 4>(c, sg, L, a, it);
         case 7: return launch_cgB_f<TY, 7>(c, sg, L, a, it);
         case 15: return launch_cgB_f<TY, 15>(c, sg, L, a, it);
-        case 47: return launch_cgB_f<TY, 47>(c, sg, L, a, it);
                  [[fallthrough]];
         case 23: if constexpr (TY == 16) return launch_cgB_f<TY, 23>(c, sg, L, a, it);
                  [[fallthrough]];
@@ -1158,13 +1156,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     c->sweep_ty = (c->cfg.sweep_rows == 4 || c->cfg.sweep_rows == 16) ? c->cfg.sweep_rows : 8;
     {   // variants built: 0-3 (memory hints), 4 and 7 (+ plane prefetch)
         const int v = c->cfg.sweep_variant & 63;
-        if ((v == 15 || v == 47) && c->sweep_ty >= 8) c->sweep_variant = v;
+        if (v == 15 && c->sweep_ty >= 8) c->sweep_variant = v;
         else if ((v == 23 || v == 31) && c->sweep_ty == 16) c->sweep_variant = v;
         else c->sweep_variant = (v & SW_PREFETCH) ? ((v & 3) == 3 ? 7 : 4) : (v & 3);
-        // experiments: CFD_HIP_SWEEP_BUFST=1 stores through st2b (variant 47)
-        if (c->sweep_variant == 15 && getenv("CFD_HIP_SWEEP_BUFST") &&
-            atoi(getenv("CFD_HIP_SWEEP_BUFST")) == 1)
-            c->sweep_variant = 47;
     }
     {
         const int vf = c->cfg.sweep_variant_fold;

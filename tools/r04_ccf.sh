@@ -9,8 +9,3 @@ tail -2 gpurun_out/${TAG}_pytest.log
 ITERS=${ITERS:-100} timeout -k 10 300 python tools/cg_variant_bench.py > gpurun_out/${TAG}.jsonl 2>gpurun_out/${TAG}.err || exit 1
 CFD_HIP_CCF=0 ITERS=${ITERS:-100} timeout -k 10 300 python tools/cg_variant_bench.py > gpurun_out/${TAG}_old.jsonl 2>>gpurun_out/${TAG}.err || exit 1
 cat gpurun_out/${TAG}.jsonl gpurun_out/${TAG}_old.jsonl
-# textbook sweeps with st2b stores (variant 47) for the A/B
-if [ -n "$BUFST" ]; then
-  CFD_HIP_SWEEP_BUFST=1 ITERS=${ITERS:-100} timeout -k 10 300 python tools/cg_variant_bench.py > gpurun_out/${TAG}_bufst.jsonl 2>>gpurun_out/${TAG}.err || exit 1
-  cat gpurun_out/${TAG}_bufst.jsonl
-fi

@@ -7,10 +7,15 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${TAG:-r02b}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+# PART=tests: the suite and smoke() only; PART=bench: the profile and the bench
+# only (one gpurun call is capped at 20 minutes)
+if [ "${PART:-all}" != "bench" ]; then
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
 rc=$?; echo "pytest exit $rc"; tail -2 gpurun_out/${TAG}_pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
 rc=$?; echo "smoke exit $rc"; tail -2 gpurun_out/${TAG}_smoke.log; [ $rc -ne 0 ] && exit $rc
+[ "${PART:-all}" = "tests" ] && exit 0
+fi
 [ -n "$NO_PROF" ] || { TAG=$TAG ARGS="--size 512 --steps 1 --warmup 1 --no-cpu-baseline --no-compare-cg-variant" bash tools/gpu_profile.sh || exit $?; \
   cp gpurun_out/prof_${TAG}/traffic.json profiles/${TAG}_traffic.json; }
 timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
