@@ -519,11 +519,11 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
         # measured HBM bytes per sweep: the committed PMC profile of these
         # kernel sources at this grid (2*FETCH_SIZE + WRITE_SIZE)
         prof = pmc_profile(n_loc)
-        def traffic_of(prefix):
+        def traffic_of(prefixes):
             if prof is None:
                 return None, None
             recs = [(k, v) for k, v in prof["kernels"].items()
-                    if k.startswith(prefix) and "hbm_bytes_per_launch" in v]
+                    if k.startswith(prefixes) and "hbm_bytes_per_launch" in v]
             if not recs:
                 return None, None
             return (round(sum(v["hbm_bytes_per_launch"] for _, v in recs) / len(recs)),
@@ -538,13 +538,18 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
             sweeps = sum(max(1, (i + 1) // 2) for i in iters)
             avg = r2ms / max(1, sweeps)
             ach = BYTES_RB2_SWEEP * n_loc / (avg * 1e-3) / 1e9
-            traffic, traffic_src = traffic_of("k_rb2")
+            traffic, traffic_src = traffic_of(("k_rb2<",))
             roof = {"bound": "hbm", "kernel": "k_rb2 (two RB-SOR iterations per sweep)",
                     "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "traffic_source": traffic_src,
                     "algorithmic_bytes": BYTES_RB2_SWEEP * n_loc,
                     "bytes_per_cell": BYTES_RB2_SWEEP, "iterations_per_sweep": 2,
+                    # what bounds it: fp64 VALU issue and the per-step barrier,
+                    # not HBM (r04 PMC at 1024^2 x 512: VALU busy ~0.5 of the
+                    # step, the XCD-contiguous tile map fetches 22 % fewer bytes
+                    # in the same time; profiles/r04_rb2_pmc_xmap*.jsonl)
+                    "limiter": "fp64 VALU issue + per-plane barrier (DESIGN.md §3 r04)",
                     "avg_sweep_ms": round(avg, 4), "sweeps": sweeps, "launches": r2n,
                     "one_iteration_sweeps": rn}
         else:
@@ -557,7 +562,7 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
             sweeps = sum(iters) + len(iters)
             avg = rms / sweeps
             ach = BYTES_RB_ITER * n_loc / (avg * 1e-3) / 1e9
-            traffic, traffic_src = traffic_of("k_rb1")
+            traffic, traffic_src = traffic_of(("k_rb1<", "k_rb1m<"))
             roof = {"bound": "hbm", "kernel": "k_rb1m (one RB-SOR sweep per launch: TC-64 tiles "
                                               "+ the narrow TC-16 strip in one grid)",
                     "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
