@@ -49,7 +49,8 @@ BYTES_SWEEP_AX = 64.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2};
                         # (the 4 pending alpha p folded; p_{it-1} is sweep A's p_old)
 BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
 BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
-BYTES_CC_FUSED = 42.0   # cg_variant 1 on one device, k_ccf: read r, p_old; write p, r (32)
+BYTES_CC_SPMV_NOW = 8.0 # cg_variant 1 on Z-slabs, k_cc2 without the w store: read r (stencil)
+BYTES_CC_FUSED = 42.0   # cg_variant 1, k_ccf: read r, p_old; write p, r (32)
                         # + the x fold's 40 B every 4th iteration (mean per iteration)
 BYTES_CG_SMALL_ITER = 64.0    # small grids, k_cg_small per iteration (x updated every iteration)
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
@@ -254,8 +255,9 @@ def main():
                               bpc_small * n_loc / (avg * 1e-3) / 1e9, small_ms)
     if small_n:  # one iteration = the solve's time / its iterations
         cg_iter_ms = small_ms / max(1, sum(iters))
-    elif args.cg_variant == 1 and "cc_fused" in sweeps:  # one launch per iteration
-        cg_iter_ms = sweeps["cc_fused"][2] or 0.0
+    elif args.cg_variant == 1 and "cc_fused" in sweeps:  # the march (+ the slab SpMV)
+        cg_iter_ms = (sweeps["cc_fused"][2] or 0.0) + (
+            (sweeps["cc_spmv"][2] or 0.0) if "cc_spmv" in sweeps else 0.0)
     elif args.cg_variant == 1:  # one iteration = update + SpMV
         cg_iter_ms = (sweeps["cc_update"][2] or 0.0) + (sweeps["cc_spmv"][2] or 0.0)
     else:  # one CG iteration = the mean of the two sweep A forms + sweep B
@@ -614,10 +616,12 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
     if cg_variant == 1 and not dist_:
         # one z-march per iteration (ccf.hpp); the timer spans the plain and
         # the fold launches, so the byte count is their mean
-        return (("cc_fused", "k_ccf<false, false>", BYTES_CC_FUSED),)
+        return (("cc_fused", "k_ccf<false, false, false>", BYTES_CC_FUSED),)
     if cg_variant == 1:
-        return (("cc_update", "k_cc1<false, false>", BYTES_CC_UPDATE),
-                ("cc_spmv", f"k_cc2<{rows}, {d}, false>", BYTES_CC_SPMV))
+        # Z-slabs: the march up to r_{it+1}, the r halo, then w = A r in
+        # registers with the one reduction (k_cc2 without the w store)
+        return (("cc_fused", "k_ccf<false, false, true>", BYTES_CC_FUSED),
+                ("cc_spmv", f"k_cc2<{rows}, {d}, false, false>", BYTES_CC_SPMV_NOW))
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
             ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, {rev}>", BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))

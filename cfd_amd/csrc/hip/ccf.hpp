@@ -50,7 +50,10 @@ struct CcfLds {
     int flag;
 };
 
-template <bool FIRST, bool FOLD>
+// NOC (Z-slabs): no stage c; p_it is also stored on the slab's halo planes
+// (the next iteration forms p there from the exchanged r), and the r halo +
+// k_cc2<..., WST = false> complete the iteration with its one reduction.
+template <bool FIRST, bool FOLD, bool NOC = false>
 static __global__ __launch_bounds__(1024, 4) void k_ccf(
     SGeo g, Lap Lp, const double* __restrict__ R0, double* __restrict__ R1,
     const double* __restrict__ Po, double* __restrict__ Pn, PPrev pv, double* __restrict__ x,
@@ -172,27 +175,33 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         rn[S1] = r1;
         __builtin_amdgcn_sched_barrier(0);
         // ---- c: w_{it+1} at q, the dot products ----
-        double2 wv;
-        stencil(LRR, rn[S0], rn[SM], r1, wv);
-        if (q >= kb && own) {
-            const double2 rc = rn[S0];
-            if (in0) {
-                accg += rc.x * rc.x;
-                accd += wv.x * rc.x;
-            }
-            if (in1) {
-                accg += rc.y * rc.y;
-                accd += wv.y * rc.y;
+        if constexpr (!NOC) {
+            double2 wv;
+            stencil(LRR, rn[S0], rn[SM], r1, wv);
+            if (q >= kb && own) {
+                const double2 rc = rn[S0];
+                if (in0) {
+                    accg += rc.x * rc.x;
+                    accd += wv.x * rc.x;
+                }
+                if (in1) {
+                    accg += rc.y * rc.y;
+                    accd += wv.y * rc.y;
+                }
             }
         }
         // ---- publish p_it (q + 2), r_{it+1} (q + 1); stores at q + 1 ----
         lput(LPW, p2);
-        lput(LRW, r1);
+        if constexpr (!NOC) lput(LRW, r1);
         {
-            const int bo = (qb >= kb && qb < ke && wr) ? col * 8 : ST_NOSTORE;
+            const bool qown = qb >= kb && qb < ke;
+            const int bo = (qown && wr) ? col * 8 : ST_NOSTORE;
+            // NOC: p also on the halo plane below / above the slab's owned planes
+            const bool qhalo = NOC && ((qb == kb - 1 && kb == g.k0) || (qb == ke && ke == g.k1));
+            const int bp = ((qown || qhalo) && wr) ? col * 8 : ST_NOSTORE;
             const long long pb = plane(qb);
             const double2 p1 = pn[S1];
-            st2b<false>(Pn + pb, g.ps, bo, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
+            st2b<false>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
             st2b<false>(R1 + pb, g.ps, bo, r1);
             if (FOLD) {
                 const double2 xo = fx[F1], qa = f0[F1], qq = f1[F1], qc = f2[F1];
@@ -215,6 +224,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     if (n < nsteps) step(IntC<0>{}, q0 + n);
     if (n + 1 < nsteps) step(IntC<1>{}, q0 + n + 1);
     if (n + 2 < nsteps) step(IntC<2>{}, q0 + n + 2);
+    if constexpr (NOC) return;  // k_cc2 reduces
     // ---- one reduction: (gamma, delta) of iteration it + 1 ----
     accg = wave_sum(accg);
     accd = wave_sum(accd);

@@ -1239,7 +1239,8 @@ __device__ __forceinline__ bool grid_sum2_last(double b0, double b1, double* par
 // w = A r on the row-pair tiling (k_cgA's stencil with p = r), written to w,
 // and the one reduction of iteration it: gamma = (r, r), delta = (w, r).
 // INIT: the w = A r_0 before iteration 0 (fin_cc0; gamma_0 comes from setup).
-template <int TY, bool DIST, bool INIT>
+// WST = false (the fused iteration on Z-slabs, ccf.hpp): w stays in registers
+template <int TY, bool DIST, bool INIT, bool WST = true>
 static __global__ __launch_bounds__(64 * TY) void k_cc2(SGeo g, Lap L,
                                                         const double* __restrict__ r,
                                                         double* __restrict__ w, CgState* st,
@@ -1281,7 +1282,7 @@ static __global__ __launch_bounds__(64 * TY) void k_cc2(SGeo g, Lap L,
         if (c.lane == 63) right = er;
         const double w0 = -lap7(L, pc.x, left, pc.y, ys.x, yn.x, pm.x, pp.x);
         const double w1 = -lap7(L, pc.y, pc.x, right, ys.y, yn.y, pm.y, pp.y);
-        if (c.act) st2(w, idx, make_double2(c.in0 ? w0 : 0.0, c.in1 ? w1 : 0.0));
+        if (WST && c.act) st2(w, idx, make_double2(c.in0 ? w0 : 0.0, c.in1 ? w1 : 0.0));
         if (c.in0) {
             accg += pc.x * pc.x;
             accd += w0 * pc.x;

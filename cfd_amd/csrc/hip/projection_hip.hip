@@ -137,45 +137,66 @@ static void launch_cc1(hip_proj_ctx* c, double* pn, const double* po, const PPre
     else launch_cc1_t<false, false>(c, pn, po, pv, x, it);
 }
 
-template <int TY, bool DIST, bool INIT>
-static void launch_cc2_t(hip_proj_ctx* c, const Lap& L, int it) {
-    hipExtLaunchKernelGGL((k_cc2<TY, DIST, INIT>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
-                          c->stream, c->ta, c->tb, 0, c->sgeo, L, c->r, c->cw, c->st, c->partials,
+template <int TY, bool DIST, bool INIT, bool WST>
+static void launch_cc2_t(hip_proj_ctx* c, const Lap& L, int it, const double* r) {
+    hipExtLaunchKernelGGL((k_cc2<TY, DIST, INIT, WST>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
+                          c->stream, c->ta, c->tb, 0, c->sgeo, L, r, c->cw, c->st, c->partials,
                           c->counter, it, c->dsum, mbox(c));
 }
 
-template <int TY>
-static void launch_cc2_ty(hip_proj_ctx* c, const Lap& L, int it, bool init) {
-    if (dist(c)) init ? launch_cc2_t<TY, true, true>(c, L, it) : launch_cc2_t<TY, true, false>(c, L, it);
-    else init ? launch_cc2_t<TY, false, true>(c, L, it) : launch_cc2_t<TY, false, false>(c, L, it);
+template <int TY, bool WST>
+static void launch_cc2_w(hip_proj_ctx* c, const Lap& L, int it, bool init, const double* r) {
+    if (dist(c)) init ? launch_cc2_t<TY, true, true, WST>(c, L, it, r)
+                      : launch_cc2_t<TY, true, false, WST>(c, L, it, r);
+    else init ? launch_cc2_t<TY, false, true, WST>(c, L, it, r)
+              : launch_cc2_t<TY, false, false, WST>(c, L, it, r);
 }
 
-static void launch_cc2(hip_proj_ctx* c, const Lap& L, int it, bool init) {
-    if (c->sweep_ty == 16) return launch_cc2_ty<16>(c, L, it, init);
-    if (c->sweep_ty == 4) return launch_cc2_ty<4>(c, L, it, init);
-    return launch_cc2_ty<8>(c, L, it, init);
+template <int TY>
+static void launch_cc2_ty(hip_proj_ctx* c, const Lap& L, int it, bool init, const double* r,
+                          bool wst) {
+    wst ? launch_cc2_w<TY, true>(c, L, it, init, r) : launch_cc2_w<TY, false>(c, L, it, init, r);
+}
+
+// w = A r (stored for k_cc1 when wst) and the iteration's one reduction
+static void launch_cc2(hip_proj_ctx* c, const Lap& L, int it, bool init, const double* r,
+                       bool wst) {
+    if (c->sweep_ty == 16) return launch_cc2_ty<16>(c, L, it, init, r, wst);
+    if (c->sweep_ty == 4) return launch_cc2_ty<4>(c, L, it, init, r, wst);
+    return launch_cc2_ty<8>(c, L, it, init, r, wst);
 }
 
 // k_ccf (ccf.hpp): cg_variant 1's whole iteration in one z-march; r_it is in
 // c->r for even it and in c->r2 for odd it
-template <bool FIRST, bool FOLD>
+// Z-slabs (NOC): the march stops after r_{it+1} (and p_it, also on the halo
+// planes); the r halo and k_cc2 (w = A r in registers, the one reduction)
+// follow
+static const double* ccf_r0(const hip_proj_ctx* c, int it) { return (it & 1) ? c->r2 : c->r; }
+static double* ccf_r1(hip_proj_ctx* c, int it) { return (it & 1) ? c->r : c->r2; }
+
+template <bool FIRST, bool FOLD, bool NOC>
 static void launch_ccf_t(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
                          const PPrev& pv, double* x, int it, int xmap) {
     const SGeo& g = c->ccgeo;
-    const double* r0 = (it & 1) ? c->r2 : c->r;
-    double* r1 = (it & 1) ? c->r : c->r2;
-    hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
-                          dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, r0, r1, po, pn, pv, x,
-                          c->st, c->partials, c->counter, it, xmap);
+    hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD, NOC>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
+                          dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, ccf_r0(c, it),
+                          ccf_r1(c, it), po, pn, pv, x, c->st, c->partials, c->counter, it, xmap);
+}
+
+template <bool NOC>
+static void launch_ccf_n(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
+                         const PPrev& pv, double* x, int it, int xmap) {
+    const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
+    if (it == 0) launch_ccf_t<true, false, NOC>(c, L, pn, po, pv, x, it, xmap);
+    else if (fold) launch_ccf_t<false, true, NOC>(c, L, pn, po, pv, x, it, xmap);
+    else launch_ccf_t<false, false, NOC>(c, L, pn, po, pv, x, it, xmap);
 }
 
 static void launch_ccf(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
                        const PPrev& pv, double* x, int it) {
     static const int xmap = getenv("CFD_HIP_CCF_XMAP") ? atoi(getenv("CFD_HIP_CCF_XMAP")) : 0;
-    const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
-    if (it == 0) launch_ccf_t<true, false>(c, L, pn, po, pv, x, it, xmap);
-    else if (fold) launch_ccf_t<false, true>(c, L, pn, po, pv, x, it, xmap);
-    else launch_ccf_t<false, false>(c, L, pn, po, pv, x, it, xmap);
+    if (dist(c)) launch_ccf_n<true>(c, L, pn, po, pv, x, it, xmap);
+    else launch_ccf_n<false>(c, L, pn, po, pv, x, it, xmap);
 }
 
 // ---------------------------------------------------------------------------
@@ -286,10 +307,10 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     // Chronopoulos-Gear (cg_variant 1): k_cc1 (pointwise) -> halo of r ->
     // k_cc2 (w = A r and both dots, ONE reduction / all-reduce)
     const bool cc = (c->cfg.cg_variant == 1);
-    // one device, 3-D: the fused iteration (k_ccf); CFD_HIP_CCF = 0 keeps
-    // k_cc1 + k_cc2 (read per solve: tests switch it)
+    // 3-D: the fused iteration (k_ccf; on Z-slabs + the r halo + k_cc2);
+    // CFD_HIP_CCF = 0 keeps k_cc1 + k_cc2 (read per solve: tests switch it)
     const char* eccf = getenv("CFD_HIP_CCF");
-    const bool ccf = cc && !D && c->ccgeo.tiles_x > 0 && !(eccf && atoi(eccf) == 0);
+    const bool ccf = cc && c->ccgeo.tiles_x > 0 && !(eccf && atoi(eccf) == 0);
     auto reduce_cc = [&](int it, bool init) -> cfd_status_t {
         if (!D || mbox(c)) return CFD_SUCCESS;
         return timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
@@ -306,22 +327,27 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];
         if (ccf) {
             timed(c, HIP_KT_CC_FUSED, [&] { launch_ccf(c, L, pnew, pold, pv, x, it); }, it);
-            return CFD_SUCCESS;
+            if (!D) return CFD_SUCCESS;
+            double* r1 = ccf_r1(c, it);
+            ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {r1}); }, it));
+            timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false, r1, false); }, it);
+            return reduce_cc(it, false);
         }
         timed(c, HIP_KT_CC_UPDATE, [&] { launch_cc1(c, pnew, pold, pv, x, it); }, it);
         if (D)
             ST_TRY(timed_span(c, c->stream, HIP_KT_HALO,
                               [&] { return halo(c, {c->r}); }, it));
-        timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false); }, it);
+        timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false, c->r, true); }, it);
         return reduce_cc(it, false);
     };
     if (cc) {
         const size_t n = field_elems(c);
-        if (!c->cw) ST_TRY(dalloc(c, &c->cw, n));
+        if (!ccf && !c->cw) ST_TRY(dalloc(c, &c->cw, n));
         if (!ccf && !c->cs) ST_TRY(dalloc(c, &c->cs, n));
         if (ccf && !c->r2) ST_TRY(dalloc(c, &c->r2, n));
-        // w_0 = A r_0 and alpha_0 (the textbook's first (p, Ap) with p_0 = r_0)
-        timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, -1, true); });
+        // w_0 = A r_0 and alpha_0 (the textbook's first (p, Ap) with p_0 =
+        // r_0); the fused iteration needs no stored w
+        timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, -1, true, c->r, !ccf); });
         ST_TRY(reduce_cc(-1, true));
     }
     auto step_it = [&](int it) { return cc ? iterate_cc(it) : iterate(it); };
@@ -1256,7 +1282,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         SGeo& cg = c->ccgeo;
         cg = rg;
         cg.tiles_x = cg.tiles_y = cg.tiles_z = 0;
-        if (c->nranks == 1 && nz >= 3 && nx >= 4 && ny >= 4) {
+        if (nz >= 3 && nx >= 4 && ny >= 4) {
             cg.xofs = 0;
             cg.tiles_x = (int)((nx - 1 + CCF_OX - 1) / CCF_OX);
             cg.tiles_y = (int)((ny - 1 + CCF_OY - 1) / CCF_OY);

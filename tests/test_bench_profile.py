@@ -28,9 +28,10 @@ def test_sweep_symbols_track_the_variant():
     one = dict((t, k) for t, k, _ in bench.sweep_kernels(16, True, 15, 0))
     assert one["cg_sweep_a"] == "k_cgA<16, false, true, 15, false>"
     assert one["cg_sweep_bx"] == "k_cgA<16, false, true, 11, true>"
-    # cg_variant 1: one fused launch per iteration on one device (k_ccf),
-    # k_cc1 + k_cc2 on Z-slabs
+    # cg_variant 1: one fused launch per iteration on one device (k_ccf); on
+    # Z-slabs the march without its last stage + k_cc2 without the w store
     cc = dict((t, k) for t, k, _ in bench.sweep_kernels(16, False, 15, 1))
-    assert cc == {"cc_fused": "k_ccf<false, false>"}
+    assert cc == {"cc_fused": "k_ccf<false, false, false>"}
     ccd = dict((t, k) for t, k, _ in bench.sweep_kernels(16, True, 15, 1))
-    assert set(ccd) == {"cc_update", "cc_spmv"}
+    assert ccd == {"cc_fused": "k_ccf<false, false, true>",
+                   "cc_spmv": "k_cc2<16, true, false, false>"}
