@@ -1286,7 +1286,10 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             cg.xofs = 0;
             cg.tiles_x = (int)((nx - 1 + CCF_OX - 1) / CCF_OX);
             cg.tiles_y = (int)((ny - 1 + CCF_OY - 1) / CCF_OY);
-            cg.kc = 128;
+            // 64-plane z runs: 1.16 vs 1.29 ms per iteration at 512^3 against
+            // 128 (684 workgroups are 2.7 rounds of 256; 16 / 32: 1.21 / 1.16,
+            // profiles/r04_ccf_kc_vs_textbook.jsonl)
+            cg.kc = 64;
             if (const char* e = getenv("CFD_HIP_CCF_KC")) cg.kc = std::max(1, atoi(e));
             while (cg.kc > 4 &&
                    (long long)cg.tiles_x * cg.tiles_y * ((nint_k + cg.kc - 1) / cg.kc) < 512)

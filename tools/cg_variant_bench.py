@@ -24,12 +24,15 @@ from cfd_amd import api  # noqa: E402
 def main():
     iters = int(os.environ.get("ITERS", "100"))
     shapes = [(512, 512, 512), (512, 512, 66)]
+    if os.environ.get("SHAPES") == "512":  # profiling runs: the cube only
+        shapes = shapes[:1]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
     rng = np.random.default_rng(1)
     for nx, ny, nz in shapes:
         rhs = np.zeros((nz, ny, nx))
         rhs[1:-1, 1:-1, 1:-1] = rng.standard_normal((nz - 2, ny - 2, nx - 2))
         h = 1.0 / (nx - 1)
-        for variant in (0, 1):
+        for variant in variants:
             ctx = api.HipProjection(nx, ny, nz, cg_variant=variant)
             prm = api._native.host().poisson_solver_params_default()
             prm.max_iterations = iters
