@@ -1286,12 +1286,14 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             cg.xofs = 0;
             cg.tiles_x = (int)((nx - 1 + CCF_OX - 1) / CCF_OX);
             cg.tiles_y = (int)((ny - 1 + CCF_OY - 1) / CCF_OY);
-            // 64-plane z runs: 1.16 vs 1.29 ms per iteration at 512^3 against
-            // 128 (684 workgroups are 2.7 rounds of 256; 16 / 32: 1.21 / 1.16,
-            // profiles/r04_ccf_kc_vs_textbook.jsonl)
-            cg.kc = 64;
-            if (const char* e = getenv("CFD_HIP_CCF_KC")) cg.kc = std::max(1, atoi(e));
-            while (cg.kc > 4 &&
+            // 32-plane z runs: 1.155-1.18 vs 1.24-1.29 ms per iteration at
+            // 512^3 against 128 (684 workgroups are 2.7 rounds of 256; 64:
+            // 1.16-1.24, 16: 1.20-1.21; profiles/r04_ccf_kc_*.jsonl)
+            cg.kc = 32;
+            const char* ekc = getenv("CFD_HIP_CCF_KC");  // experiments
+            if (ekc) cg.kc = std::max(1, atoi(ekc));
+            const bool kc_fixed = getenv("CFD_HIP_CCF_KC_FIXED") != nullptr;
+            while (!kc_fixed && cg.kc > 4 &&
                    (long long)cg.tiles_x * cg.tiles_y * ((nint_k + cg.kc - 1) / cg.kc) < 512)
                 cg.kc /= 2;
             cg.kc = std::max(1, std::min(cg.kc, nint_k));

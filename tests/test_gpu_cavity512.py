@@ -128,6 +128,32 @@ def test_cavity512_trajectory_vs_oracle(hip_lib):
     print("cavity512 largest deviations from the oracle:", worst)
 
 
+@pytest.mark.timeout(600)
+def test_cavity512_single_reduction_cg_vs_oracle(hip_lib):
+    """The north star's single-reduction CG (cg_variant 1: one reduction per
+    iteration, on one device the fused march k_ccf) on the same trajectory,
+    steps 1-6, against the textbook-CG oracle at the single-device bars
+    (it is the same Krylov method with other rounding: the iteration counts
+    come out identical, profiles/r04_cc_cavity512_vs_oracle.jsonl)."""
+    rec = _fixture()
+    g = api.Grid(N, N, N, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
+    params = api.validation_params(rec["dt"], 1.0 / rec["re"])
+    ctx = api.HipProjection(N, N, N, cg_variant=1)
+    try:
+        _init(ctx)
+        worst = {"norm_rel": 0.0, "plane_rel": 0.0}
+        for row in rec["steps"][:6]:
+            st = A.SolverStats()
+            s = ctx.step_device(g, params, st)
+            assert s == A.CFD_SUCCESS, (row["step"], s, api._native.last_error())
+            ps = ctx.poisson_stats()
+            check_step(row, ps.iterations, ps.initial_residual, ps.final_residual,
+                       st.max_velocity, st.max_pressure, lambda k: ctx.get_field(FIDS[k]), worst)
+    finally:
+        ctx.close()
+    print("cavity512 single-reduction CG, largest deviations from the oracle:", worst)
+
+
 @pytest.mark.timeout(900)
 def test_cavity512_slabs8_vs_oracle(hip_lib, monkeypatch):
     """configs[3]'s decomposition at its real slab depth (VERDICT r03 item
