@@ -78,8 +78,18 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     const int r = w + 16 * (lane >> 5);
     const int i0 = tx * CCF_OX - 2 + 2 * c;  // even; the pair is (i0, i0 + 1)
     const int j = ty * CCF_OY - 2 + r;
-    const int kb = g.k0 + tz * g.kc;
-    const int ke = min(kb + g.kc, g.k1);
+    // kmode 1 (Z-slabs, NOC): the slab's two edge planes (tz 0 -> k0, tz 1 ->
+    // k1 - 1); kmode 2: the planes [kt0, kt1) between them
+    int kb, ke;
+    if (g.kmode == 1) {
+        kb = (tz == 0) ? g.k0 : g.k1 - 1;
+        ke = kb + 1;
+    } else {
+        const int kt0 = (g.kmode == 2) ? g.kt0 : g.k0;
+        const int kt1 = (g.kmode == 2) ? g.kt1 : g.k1;
+        kb = kt0 + tz * g.kc;
+        ke = min(kb + g.kc, kt1);
+    }
     const bool jin = j >= 1 && j <= g.ny - 2;
     const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;
     const bool in1 = jin && i0 + 1 >= 1 && i0 + 1 <= g.nx - 2;

@@ -134,6 +134,7 @@ struct hip_proj_ctx {
     RxState* rxst2 = nullptr;            // scratch state of k_rb2's recompute sweeps
     SGeo r2geo{};                        // two-iterations-per-sweep RB-SOR tiling (k_rb2)
     SGeo ccgeo{};                        // fused single-reduction CG tiling (k_ccf)
+    SGeo cc_edge{}, cc_int{};            // slabs: k_ccf on the edge planes, then the rest
     double* r2 = nullptr;                // k_ccf: r_{it+1} when r_it is in r (by parity)
     double* partials = nullptr;
     unsigned* counter = nullptr;

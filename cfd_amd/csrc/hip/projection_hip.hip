@@ -175,28 +175,28 @@ static const double* ccf_r0(const hip_proj_ctx* c, int it) { return (it & 1) ? c
 static double* ccf_r1(hip_proj_ctx* c, int it) { return (it & 1) ? c->r : c->r2; }
 
 template <bool FIRST, bool FOLD, bool NOC>
-static void launch_ccf_t(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
-                         const PPrev& pv, double* x, int it, int xmap) {
-    const SGeo& g = c->ccgeo;
+static void launch_ccf_t(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
+                         const double* po, const PPrev& pv, double* x, int it, int xmap) {
     hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD, NOC>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
                           dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, ccf_r0(c, it),
                           ccf_r1(c, it), po, pn, pv, x, c->st, c->partials, c->counter, it, xmap);
 }
 
 template <bool NOC>
-static void launch_ccf_n(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
-                         const PPrev& pv, double* x, int it, int xmap) {
+static void launch_ccf_n(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
+                         const double* po, const PPrev& pv, double* x, int it, int xmap) {
     const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
-    if (it == 0) launch_ccf_t<true, false, NOC>(c, L, pn, po, pv, x, it, xmap);
-    else if (fold) launch_ccf_t<false, true, NOC>(c, L, pn, po, pv, x, it, xmap);
-    else launch_ccf_t<false, false, NOC>(c, L, pn, po, pv, x, it, xmap);
+    if (it == 0) launch_ccf_t<true, false, NOC>(c, g, L, pn, po, pv, x, it, xmap);
+    else if (fold) launch_ccf_t<false, true, NOC>(c, g, L, pn, po, pv, x, it, xmap);
+    else launch_ccf_t<false, false, NOC>(c, g, L, pn, po, pv, x, it, xmap);
 }
 
-static void launch_ccf(hip_proj_ctx* c, const Lap& L, double* pn, const double* po,
-                       const PPrev& pv, double* x, int it) {
+// g: c->ccgeo (the whole march), or on Z-slabs c->cc_edge / c->cc_int
+static void launch_ccf(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
+                       const double* po, const PPrev& pv, double* x, int it) {
     static const int xmap = getenv("CFD_HIP_CCF_XMAP") ? atoi(getenv("CFD_HIP_CCF_XMAP")) : 0;
-    if (dist(c)) launch_ccf_n<true>(c, L, pn, po, pv, x, it, xmap);
-    else launch_ccf_n<false>(c, L, pn, po, pv, x, it, xmap);
+    if (dist(c)) launch_ccf_n<true>(c, g, L, pn, po, pv, x, it, xmap);
+    else launch_ccf_n<false>(c, g, L, pn, po, pv, x, it, xmap);
 }
 
 // ---------------------------------------------------------------------------
@@ -325,11 +325,33 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         double* pold = P[(it + CG_XFOLD - 1) % CG_XFOLD];
         PPrev pv;
         for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];
+        if (ccf && !D) {
+            timed(c, HIP_KT_CC_FUSED, [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it); },
+                  it);
+            return CFD_SUCCESS;
+        }
         if (ccf) {
-            timed(c, HIP_KT_CC_FUSED, [&] { launch_ccf(c, L, pnew, pold, pv, x, it); }, it);
-            if (!D) return CFD_SUCCESS;
+            // Z-slabs: r_{it+1} on the two edge planes first; its halo then
+            // travels on the side stream (halo communicator) while the march
+            // covers the interior planes; the SpMV + reduction wait for it
             double* r1 = ccf_r1(c, it);
-            ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {r1}); }, it));
+            if (c->cc_edge.tiles_x > 0) {
+                launch_ccf(c, c->cc_edge, L, pnew, pold, pv, x, it);
+                HIP_TRY(hipEventRecord(c->ev_b, c->stream));
+                HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
+                double* rr[1] = {r1};
+                ST_TRY(timed_span(c, c->hstream, HIP_KT_HALO, [&] {
+                    return c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false);
+                }, it));
+                HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
+                timed(c, HIP_KT_CC_FUSED,
+                      [&] { launch_ccf(c, c->cc_int, L, pnew, pold, pv, x, it); }, it);
+                HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
+            } else {
+                timed(c, HIP_KT_CC_FUSED,
+                      [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it); }, it);
+                ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {r1}); }, it));
+            }
             timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false, r1, false); }, it);
             return reduce_cc(it, false);
         }
@@ -1299,6 +1321,23 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             cg.kc = std::max(1, std::min(cg.kc, nint_k));
             cg.tiles_z = (nint_k + cg.kc - 1) / cg.kc;
             n_partials = std::max(n_partials, cg.tiles_x * cg.tiles_y * cg.tiles_z);
+            // Z-slabs of >= 3 planes: the edge planes' launch (kmode 1) and
+            // the interior planes' (kmode 2), so the r halo overlaps the latter
+            c->cc_edge = c->cc_int = cg;
+            c->cc_edge.tiles_x = c->cc_int.tiles_x = 0;
+            if (c->nranks > 1 && nint_k >= 3) {
+                SGeo& e = c->cc_edge;
+                SGeo& m = c->cc_int;
+                e = m = cg;
+                e.kmode = 1;
+                e.kc = 1;
+                e.tiles_z = 2;
+                m.kmode = 2;
+                m.kt0 = cg.k0 + 1;
+                m.kt1 = cg.k1 - 1;
+                m.kc = std::max(1, std::min(cg.kc, m.kt1 - m.kt0));
+                m.tiles_z = (m.kt1 - m.kt0 + m.kc - 1) / m.kc;
+            }
         }
         // the last x tile of a TC-64 launch is partial unless 124 divides the
         // row: its workgroups run a full tile's steps for a few columns
