@@ -97,9 +97,11 @@ def parse():
                     help="CG sweep variant: bit0 NT stores, bit1 NT loads, bit2 plane prefetch, "
                          "bit3 one edge load (built: 0-4, 7, 15, and 23 / 31 with 16 rows; "
                          "default 15, or CFD_BENCH_SWEEP_VARIANT)")
-    ap.add_argument("--cg-variant", type=int, default=0, choices=(0, 1),
+    ap.add_argument("--cg-variant", type=int, default=-1, choices=(-1, 0, 1),
                     help="0: textbook CG (the reference's loop); 1: single-reduction "
-                         "(Chronopoulos-Gear) CG")
+                         "(Chronopoulos-Gear) CG, one fused z-march per iteration; -1 "
+                         "(default): 1 on one GPU at n >= 512, where it is measured faster "
+                         "(DESIGN.md section 5), else 0")
     ap.add_argument("--no-compare-cg-variant", action="store_true",
                     help="skip the side measurement of the other CG variant after the "
                          "timed region")
@@ -189,6 +191,8 @@ def main():
         c.synchronize()
         return c
 
+    if args.cg_variant < 0:
+        args.cg_variant = cg_variant_auto(n, world)
     ctx = make_ctx(args.cg_variant)
 
     def step():
@@ -273,16 +277,18 @@ def main():
     traffic = traffic_src = measured_gbps = None
     measured_from = []
     if prof is not None:
-        bpl = prof["kernels"].get(kname, {}).get("hbm_bytes_per_launch")
+        bpl = (prof_record(prof, kname) or {}).get("hbm_bytes_per_launch")
         traffic = round(bpl) if bpl else None
-        traffic_src = prof["file"] + ": " + kname if bpl else None
+        traffic_src = (prof["file"] + ": " + ("k_ccf<*, *, false> (launch-weighted)"
+                                              if kname == "k_ccf<false, false, false>"
+                                              else kname)) if bpl else None
         names = {k: v[0] for k, v in sweeps.items()}
         tot = 0.0
         for key, (ms, cnt) in kt.items():
             if not cnt:
                 continue
             kn = names.get(key) or TIMER_KERNEL.get(key)
-            rec = prof["kernels"].get(kn) if kn else None
+            rec = prof_record(prof, kn) if kn else None
             if rec and "hbm_bytes_per_launch" in rec:
                 tot += rec["hbm_bytes_per_launch"] * cnt
                 measured_from.append(kn)
@@ -625,6 +631,31 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
             ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, {rev}>", BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))
+
+
+def cg_variant_auto(n, world):
+    """The bench's CG variant: the single-reduction z-march (k_ccf) where it is
+    measured faster than textbook CG, i.e. one GPU at 512^3 (1.17 vs 1.31 ms
+    per iteration); on the slab shapes of 2 / 4 / 8 ranks it is even or
+    slower (0.638 vs 0.645, 0.342 vs 0.324, 0.190 vs 0.162 ms: fewer z runs
+    leave the last round of workgroups part-empty), so slabs keep textbook CG
+    (profiles/r04_ccf_slab_shapes.jsonl)."""
+    return 1 if world == 1 and n >= 512 else 0
+
+
+def prof_record(prof, kname):
+    """PMC record of a timer's kernel. The one-device single-reduction timer
+    spans k_ccf's first, plain and fold launches (k_ccf<*, *, false>): their
+    bytes per launch averaged over the profiled launch counts."""
+    if kname == "k_ccf<false, false, false>":
+        recs = [v for k, v in prof["kernels"].items()
+                if k.startswith("k_ccf<") and k.endswith(", false>")
+                and "hbm_bytes_per_launch" in v and v.get("calls")]
+        n = sum(v["calls"] for v in recs)
+        if n:
+            return {"hbm_bytes_per_launch":
+                    sum(v["hbm_bytes_per_launch"] * v["calls"] for v in recs) / n}
+    return prof["kernels"].get(kname)
 
 
 def pmc_profile(cells):

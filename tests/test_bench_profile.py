@@ -14,14 +14,33 @@ def test_profile_is_current_and_complete():
     if prof is None:
         pytest.xfail("no PMC profile of the current cfd_amd/csrc/hip sources: "
                      "re-run tools/gpu_profile.sh and commit its traffic.json")
-    have = prof["kernels"]
-    # the default run: 1 rank, 16-row sweeps, variant 15, textbook CG
-    want = [k for _, k, _ in bench.sweep_kernels(16, False, 15, 0)]
+    # the default run: 1 rank at 512^3, 16-row sweeps, variant 15, the CG
+    # variant bench.cg_variant_auto picks there (single-reduction)
+    variant = bench.cg_variant_auto(512, 1)
+    assert variant == 1
+    want = [k for _, k, _ in bench.sweep_kernels(16, False, 15, variant)]
     want += list(bench.TIMER_KERNEL.values())
-    missing = [k for k in want if "hbm_bytes_per_launch" not in have.get(k, {})]
+    recs = {k: bench.prof_record(prof, k) or {} for k in want}
+    missing = [k for k, r in recs.items() if "hbm_bytes_per_launch" not in r]
     assert not missing, missing
     for k in want:
-        assert have[k]["hbm_bytes_per_launch"] > 0
+        assert recs[k]["hbm_bytes_per_launch"] > 0
+
+
+def test_cg_variant_auto_and_fused_record():
+    # single-reduction only where it is measured faster: one GPU at 512^3
+    assert bench.cg_variant_auto(512, 1) == 1
+    assert bench.cg_variant_auto(256, 1) == 0
+    assert all(bench.cg_variant_auto(512, w) == 0 for w in (2, 4, 8))
+    # the fused timer's bytes: launch-weighted over k_ccf<*, *, false> only
+    prof = {"kernels": {
+        "k_ccf<true, false, false>": {"calls": 1, "hbm_bytes_per_launch": 10.0},
+        "k_ccf<false, false, false>": {"calls": 5, "hbm_bytes_per_launch": 20.0},
+        "k_ccf<false, true, false>": {"calls": 2, "hbm_bytes_per_launch": 50.0},
+        "k_ccf<false, false, true>": {"calls": 9, "hbm_bytes_per_launch": 999.0}}}
+    rec = bench.prof_record(prof, "k_ccf<false, false, false>")
+    assert rec["hbm_bytes_per_launch"] == pytest.approx((10 + 100 + 100) / 8)
+    assert bench.prof_record(prof, "k_ccf<false, false, true>")["hbm_bytes_per_launch"] == 999.0
 
 
 def test_sweep_symbols_track_the_variant():

@@ -47,6 +47,24 @@ def test_bench_one_gpu_contract(hip_lib):
     assert d["cg_sweeps"]["cg_sweep_bx"]["kernel"].startswith("k_cgA<")  # the fold sweep
 
 
+def test_bench_512_single_reduction_default(hip_lib):
+    """At 512^3 on one GPU the default CG is the single-reduction z-march
+    (bench.cg_variant_auto); its line carries k_ccf's roofline and the textbook
+    iteration beside it."""
+    r = subprocess.run([sys.executable, "bench.py", "--size", "512", "--steps", "1", "--warmup",
+                        "0", "--no-cpu-baseline"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["cg_variant"] == 1 and d["value"] > 0
+    assert d["roofline"]["kernel"] == "k_ccf<false, false, false>"
+    assert d["roofline"]["bytes_per_cell"] == 42.0 and 0 < d["roofline"]["frac"] < 1
+    assert d["cg_iters_per_step"][0] > 0 and d["cg_iter_ms"] > 0
+    cmp = d["cg_variant_compare"]
+    assert cmp["cg_variant"] == 0 and cmp["cg_iters"] > 0
+
+
 @pytest.mark.parametrize("case,world,size", [("cavity", 2, 66), ("tg", 2, 66), ("cavity", 4, 66),
                                              ("cavity", 8, 130)])
 def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
