@@ -21,4 +21,22 @@ def hip_lib():
     from cfd_amd import _native
     lib = _native.hip()
     assert lib.hip_projection_available() == 1, "no HIP device visible to libcfd_hip.so"
+    _install_native_backtrace()
     return lib
+
+
+def _install_native_backtrace():
+    """On a host segfault, print the native frames before faulthandler's
+    Python ones (tests/native/segv_bt.c, built into /tmp on first use)."""
+    import ctypes
+    import subprocess
+    import tempfile
+
+    src = ROOT / "tests" / "native" / "segv_bt.c"
+    out = Path(tempfile.gettempdir()) / f"cfd_segv_bt_{os.getpid()}.so"
+    try:
+        subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-o", str(out), str(src)], check=True,
+                       capture_output=True, timeout=60)
+        ctypes.CDLL(str(out)).segv_bt_install()
+    except (OSError, subprocess.SubprocessError):
+        pass  # a diagnostic aid only
