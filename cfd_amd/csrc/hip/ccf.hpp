@@ -140,16 +140,11 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     const double2 zero = make_double2(0.0, 0.0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) pn[s] = rn[s] = po[s] = rr[s] = zero;
+    fx[0] = fx[1] = f0[0] = f0[1] = f1[0] = f1[1] = f2[0] = f2[1] = zero;
     rr[1] = ld2(R0, plane(q0 + 1) + col);
     rr[2] = ld2(R0, plane(q0 + 2) + col);
     if (!FIRST) po[2] = ld2(Po, plane(q0 + 2) + col);
-    if (FOLD) {
-        const long long o = plane(q0 + 1) + col;
-        fx[1] = ld2(x, o);
-        f0[1] = ld2(pv.q[0], o);
-        f1[1] = ld2(pv.q[1], o);
-        f2[1] = ld2(pv.q[2], o);
-    }
+    // (the fold operands of plane q0 + 1 = kb - 3 are never stored: no load)
     double accg = 0.0, accd = 0.0;
     auto step = [&](auto Pc, int q) __attribute__((always_inline)) {
         constexpr int P = decltype(Pc)::value;
@@ -163,7 +158,10 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         // 512^3, profiles/r04_ccf_prefetch2_cg_variant.jsonl)
         rr[S3] = ld2(R0, plane(q + 3) + col);
         if (!FIRST) po[S3] = ld2(Po, plane(q + 3) + col);
-        if (FOLD) {
+        if (FOLD && wr && q + 2 >= kb && q + 2 < ke) {
+            // only the lanes and planes that store x read its operands (the
+            // halo lanes' and planes' loads would be re-fetched lines): 1.123
+            // vs 1.159 ms per iteration at 512^3, profiles/r04_ccf_fold_owned_loads_ab.jsonl
             const long long o = plane(q + 2) + col;
             fx[F2] = ld2(x, o);
             f0[F2] = ld2(pv.q[0], o);
