@@ -32,6 +32,7 @@ def test_cg_variant_auto_and_fused_record():
     assert bench.cg_variant_auto(512, 1) == 1
     assert bench.cg_variant_auto(256, 1) == 0
     assert all(bench.cg_variant_auto(512, w) == 0 for w in (2, 4, 8))
+    assert bench.cg_variant_auto(512, 1, "tg") == 0
     # the fused timer's bytes: launch-weighted over k_ccf<*, *, false> only
     prof = {"kernels": {
         "k_ccf<true, false, false>": {"calls": 1, "hbm_bytes_per_launch": 10.0},
