@@ -141,7 +141,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
 #pragma unroll
     for (int s = 0; s < 4; ++s) pn[s] = rn[s] = po[s] = rr[s] = zero;
     fx[0] = fx[1] = f0[0] = f0[1] = f1[0] = f1[1] = f2[0] = f2[1] = zero;
-    rr[1] = ld2(R0, plane(q0 + 1) + col);
+    // (r_it of plane q0 + 1 = kb - 3 only feeds r_{it+1} there, never used)
     rr[2] = ld2(R0, plane(q0 + 2) + col);
     if (!FIRST) po[2] = ld2(Po, plane(q0 + 2) + col);
     // (the fold operands of plane q0 + 1 = kb - 3 are never stored: no load)
@@ -156,8 +156,12 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         // prefetch plane q + 3 (r_it, p_{it-1}) and the fold operands of q + 2
         // (two steps ahead measured slower: 1.32 vs 1.27 ms per iteration at
         // 512^3, profiles/r04_ccf_prefetch2_cg_variant.jsonl)
-        rr[S3] = ld2(R0, plane(q + 3) + col);
-        if (!FIRST) po[S3] = ld2(Po, plane(q + 3) + col);
+        if (q + 1 < ke) {  // the last step has no next step to load for
+            // (skipping the two unused edge-plane loads: 1.157 -> 1.119 ms per
+            // iteration at 512^3, profiles/r04_ccf_edge_plane_loads_ab.jsonl)
+            rr[S3] = ld2(R0, plane(q + 3) + col);
+            if (!FIRST) po[S3] = ld2(Po, plane(q + 3) + col);
+        }
         if (FOLD && wr && q + 2 >= kb && q + 2 < ke) {
             // only the lanes and planes that store x read its operands (the
             // halo lanes' and planes' loads would be re-fetched lines): 1.123
