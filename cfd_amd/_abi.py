@@ -43,6 +43,7 @@ KERNEL_TIMERS = ["predictor", "cg_setup", "cg_sweep_a", "cg_sweep_b", "corrector
                  "relax", "residual", "energy", "rk_stage", "cg_sweep_bx", "cc_update",
                  "cc_spmv", "halo", "allreduce", "cg_small", "relax2", "cc_fused"]
 HIP_KT_COUNT = len(KERNEL_TIMERS)
+HIP_PROJ_ABI_VERSION = 2  # projection_hip.h
 
 # oracle_poisson_kind_t
 ORACLE_POISSON_CG = 0

@@ -18,6 +18,7 @@ import threading
 from pathlib import Path
 
 from . import _abi as A
+from . import _sha
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_DIR = PKG_DIR / "lib"
@@ -44,20 +45,29 @@ def build(force: bool = False, jobs: int = 4) -> None:
 def kernel_source_sha() -> str:
     """sha256 over the HIP sources (csrc/hip/*.hip, *.hpp) the built library
     came from: PMC profiles record it, bench.py uses a profile's byte counts
-    only for the same kernels."""
-    import hashlib
-
-    h = hashlib.sha256()
-    for f in sorted((CSRC_DIR / "hip").glob("*.hip")) + sorted((CSRC_DIR / "hip").glob("*.hpp")):
-        h.update(f.name.encode())
-        h.update(f.read_bytes())
-    return h.hexdigest()[:16]
+    only for the same kernels (the loader guarantees the library was built
+    from these sources, see _check_build_id)."""
+    return _sha.kernel_source_sha()
 
 
 def _ensure_built() -> None:
     if HIP_LIB.exists() and HOST_LIB.exists():
         return
     build()
+
+
+def _check_build_id(lib) -> None:
+    """Refuse a libcfd_hip.so built from other sources than the ones beside it
+    (a stale build would run old kernels under the new sources' name, and
+    bench.py would charge it the new kernels' PMC bytes). CFD_AMD_HIP_LIB (an
+    explicitly chosen other build, A/B experiments) skips the check."""
+    if os.environ.get("CFD_AMD_HIP_LIB"):
+        return
+    got = lib.hip_proj_build_id().decode()
+    want = _sha.library_source_sha()
+    if got != want:
+        raise RuntimeError(f"{HIP_LIB} was built from other sources (build id {got}, sources "
+                           f"{want}): rebuild it with `make -C {CSRC_DIR}`")
 
 
 def _sig(lib, name, restype, *argtypes):
@@ -178,6 +188,9 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_enable_timing", None, V, C.c_int)
     _sig(lib, "hip_proj_reset_timing", None, V)
     _sig(lib, "hip_proj_get_timing", None, V, A.c_double_p, P(C.c_longlong))
+    _sig(lib, "hip_proj_get_timing_n", C.c_int, V, A.c_double_p, P(C.c_longlong), C.c_int)
+    _sig(lib, "hip_proj_abi_version", C.c_int)
+    _sig(lib, "hip_proj_build_id", C.c_char_p)
     _sig(lib, "hip_proj_synchronize", C.c_int, V)
     _sig(lib, "hip_proj_sync_host", C.c_int, V, P(A.FlowField))
     _sig(lib, "hip_proj_mark_host_dirty", C.c_int, V)
@@ -279,6 +292,10 @@ def hip():
             _import_torch_first()
             lib = C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL)
             _bind_hip(lib)
+            _check_build_id(lib)
+            if lib.hip_proj_abi_version() != A.HIP_PROJ_ABI_VERSION:
+                raise RuntimeError(f"{HIP_LIB}: ABI version {lib.hip_proj_abi_version()}, "
+                                   f"the bindings expect {A.HIP_PROJ_ABI_VERSION}")
             _hip = lib
         return _hip
 

@@ -570,7 +570,7 @@ class HipProjection:
     def timing(self):
         ms = (C.c_double * A.HIP_KT_COUNT)()
         n = (C.c_longlong * A.HIP_KT_COUNT)()
-        self._lib().hip_proj_get_timing(self._ctx, ms, n)
+        self._lib().hip_proj_get_timing_n(self._ctx, ms, n, A.HIP_KT_COUNT)
         return {name: (ms[i], n[i]) for i, name in enumerate(A.KERNEL_TIMERS)}
 
     def synchronize(self):

@@ -1754,15 +1754,24 @@ void hip_proj_reset_timing(hip_proj_ctx_t* c) {
     }
 }
 
-void hip_proj_get_timing(hip_proj_ctx_t* c, double* total_ms, long long* launches) {
-    if (!c) return;
+int hip_proj_get_timing_n(hip_proj_ctx_t* c, double* total_ms, long long* launches,
+                          int capacity) {
+    if (!c || capacity <= 0) return 0;
     hipStreamSynchronize(c->stream);
     flush_timing(c);
-    for (int k = 0; k < HIP_KT_COUNT; k++) {
+    const int n = std::min(capacity, (int)HIP_KT_COUNT);
+    for (int k = 0; k < n; k++) {
         if (total_ms) total_ms[k] = c->kt_ms[k];
         if (launches) launches[k] = c->kt_n[k];
     }
+    return n;
 }
+
+void hip_proj_get_timing(hip_proj_ctx_t* c, double* total_ms, long long* launches) {
+    (void)hip_proj_get_timing_n(c, total_ms, launches, HIP_KT_COUNT_V1);
+}
+
+int hip_proj_abi_version(void) { return HIP_PROJ_ABI_VERSION; }
 
 }  // extern "C"
 

@@ -556,11 +556,12 @@ static const char* const s_solver_names[] = {
     "explicit_euler", "explicit_euler_optimized", "projection", "projection_optimized",
     "explicit_euler_gpu", "projection_gpu", "explicit_euler_omp", "projection_omp",
     "projection_hip", "projection_hip_rbsor", "projection_hip_jacobi", "rk4_hip",
+    "projection_hip_cg1",
 };
 
 int simulation_list_solvers(const char** names, int max_count) {
     const int total = (int)(sizeof(s_solver_names) / sizeof(s_solver_names[0]));
-    const int n = g_hip_patch ? total : total - 4;
+    const int n = g_hip_patch ? total : total - 5;
     if (names && max_count > 0) {
         int fill = n < max_count ? n : max_count;
         for (int i = 0; i < fill; i++) names[i] = s_solver_names[i];

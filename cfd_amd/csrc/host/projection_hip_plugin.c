@@ -54,6 +54,11 @@ static int method_of(const ns_solver_t* solver) {
     return HIP_POISSON_CG;
 }
 
+/* projection_hip_cg1: the single-reduction CG (cg_variant 1) */
+static int cg_variant_of(const ns_solver_t* solver) {
+    return (solver->name && strcmp(solver->name, NS_SOLVER_TYPE_PROJECTION_HIP_CG1) == 0) ? 1 : 0;
+}
+
 static cfd_status_t get_ctx(ns_solver_t* solver, const grid* g, hip_proj_ctx_t** out) {
     plugin_ctx* pc = (plugin_ctx*)solver->context;
     if (!pc) {
@@ -70,6 +75,7 @@ static cfd_status_t get_ctx(ns_solver_t* solver, const grid* g, hip_proj_ctx_t**
     if (!pc->ctx) {
         hip_proj_config_t cfg = hip_proj_config_default();
         cfg.poisson_method = method_of(solver);
+        cfg.cg_variant = cg_variant_of(solver);
         if (cfg.poisson_method == HIP_POISSON_JACOBI) cfg.poisson_max_iter = 2000; /* linear_solver.c:274-276 */
         /* CFD_HIP_DIRTY_FACES=N: the resident mode of `step` with a full
          * download every N steps (the driver's output interval), see
@@ -175,6 +181,12 @@ ns_solver_t* create_projection_hip_jacobi_solver(void) {
                        "Projection method with Jacobi pressure solve (HIP, MI355X)");
 }
 
+ns_solver_t* create_projection_hip_cg1_solver(void) {
+    return make_solver(NS_SOLVER_TYPE_PROJECTION_HIP_CG1,
+                       "Projection method with single-reduction CG pressure solve "
+                       "(Chronopoulos-Gear, one all-reduce per iteration; HIP, MI355X)");
+}
+
 /* rk4_hip: rk4_step / rk4_solve (solver_registry.c:748-800) on the device */
 ns_solver_t* create_rk4_hip_solver(void) {
     return make_solver(NS_SOLVER_TYPE_RK4_HIP, "RK4 time integration (HIP, MI355X)");
@@ -188,4 +200,6 @@ void cfd_hip_register_solvers(ns_solver_registry_t* registry) {
     cfd_registry_register(registry, NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI,
                           create_projection_hip_jacobi_solver);
     cfd_registry_register(registry, NS_SOLVER_TYPE_RK4_HIP, create_rk4_hip_solver);
+    cfd_registry_register(registry, NS_SOLVER_TYPE_PROJECTION_HIP_CG1,
+                          create_projection_hip_cg1_solver);
 }

@@ -12,7 +12,10 @@
  *     unchanged through init_simulation* / run_simulation_step / solver_step.
  *     `projection_hip_rbsor` and `projection_hip_jacobi` select the Red-Black
  *     SOR / Jacobi pressure solver instead of CG (the reference hard-codes CG
- *     in the projection, solver_projection.c:217-218).
+ *     in the projection, solver_projection.c:217-218). `projection_hip_cg1`
+ *     runs the single-reduction (Chronopoulos-Gear) CG, hip_proj_config_t
+ *     .cg_variant = 1: the same stopping rule and stats, one reduction per
+ *     iteration, iterates equal to textbook CG's up to rounding.
  *
  *  2. The thin context API (`hip_proj_*`) the plugin calls. It owns all
  *     device memory, so it also serves device-resident drivers (bench.py,
@@ -37,6 +40,7 @@ extern "C" {
 #define NS_SOLVER_TYPE_PROJECTION_HIP        "projection_hip"
 #define NS_SOLVER_TYPE_PROJECTION_HIP_RBSOR  "projection_hip_rbsor"
 #define NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI "projection_hip_jacobi"
+#define NS_SOLVER_TYPE_PROJECTION_HIP_CG1    "projection_hip_cg1"
 #define NS_SOLVER_TYPE_RK4_HIP               "rk4_hip"
 
 /* Pressure-Poisson method used inside the HIP projection step. */
@@ -218,8 +222,28 @@ CFD_HIP_EXPORT cfd_status_t hip_proj_get_poisson_stats(hip_proj_ctx_t* ctx,
 /* Kernel timing with HIP events on the context's stream. */
 CFD_HIP_EXPORT void hip_proj_enable_timing(hip_proj_ctx_t* ctx, int enable);
 CFD_HIP_EXPORT void hip_proj_reset_timing(hip_proj_ctx_t* ctx);
-/* total_ms[k] and launches[k] for each hip_kernel_timer_t k. */
+/* total_ms[k] and launches[k] for k < min(capacity, HIP_KT_COUNT); returns the
+ * number of entries written (arrays may be NULL). Callers size their arrays
+ * with the HIP_KT_COUNT of the header they were built against. */
+CFD_HIP_EXPORT int hip_proj_get_timing_n(hip_proj_ctx_t* ctx, double* total_ms,
+                                         long long* launches, int capacity);
+/* Legacy getter without a capacity: writes the first HIP_KT_COUNT_V1 (15)
+ * entries only, the count of the header it was first published with, so a
+ * caller built against that header is never overrun. Use hip_proj_get_timing_n. */
+#define HIP_KT_COUNT_V1 15
 CFD_HIP_EXPORT void hip_proj_get_timing(hip_proj_ctx_t* ctx, double* total_ms, long long* launches);
+
+/* ABI version of this header (bumped when a struct layout, an enum's count or
+ * a signature changes) and of the loaded library: a caller checks
+ * hip_proj_abi_version() == HIP_PROJ_ABI_VERSION. Version 2: HIP_KT_COUNT 17,
+ * hip_proj_get_timing_n, projection_hip_cg1. */
+#define HIP_PROJ_ABI_VERSION 2
+CFD_HIP_EXPORT int hip_proj_abi_version(void);
+/* sha256 prefix (16 hex digits) of the sources the library was built from
+ * (cfd_amd/_sha.py: csrc/hip, csrc/host, include/cfd_hip), embedded at
+ * build time; the Python loader refuses a library whose id differs from the
+ * sources beside it. */
+CFD_HIP_EXPORT const char* hip_proj_build_id(void);
 
 CFD_HIP_EXPORT cfd_status_t hip_proj_synchronize(hip_proj_ctx_t* ctx);
 /* Bytes of device memory held by the context. */
@@ -387,6 +411,7 @@ CFD_HIP_EXPORT cfd_status_t hip_rk4_step(hip_proj_ctx_t* ctx, flow_field* field,
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_rbsor_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_projection_hip_jacobi_solver(void);
+CFD_HIP_EXPORT ns_solver_t* create_projection_hip_cg1_solver(void);
 CFD_HIP_EXPORT ns_solver_t* create_rk4_hip_solver(void);
 /* poisson_solver_t GPU backend factories under the reference's names
  * (linear_solver_internal.h:54-57; reached via poisson_solver_create(method,
@@ -395,7 +420,7 @@ CFD_HIP_EXPORT ns_solver_t* create_rk4_hip_solver(void);
 CFD_HIP_EXPORT poisson_solver_t* create_cg_gpu_solver(void);
 CFD_HIP_EXPORT poisson_solver_t* create_redblack_gpu_solver(void);
 CFD_HIP_EXPORT poisson_solver_t* create_jacobi_gpu_solver(void);
-/* Registers the four names above through cfd_registry_register(). */
+/* Registers the five names above through cfd_registry_register(). */
 CFD_HIP_EXPORT void cfd_hip_register_solvers(ns_solver_registry_t* registry);
 
 #ifdef __cplusplus

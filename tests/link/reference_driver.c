@@ -42,8 +42,9 @@ static int contains(const char** names, int n, const char* want) {
 
 int main(void) {
     cfd_init();
-    const char* hip_names[4] = {NS_SOLVER_TYPE_PROJECTION_HIP, NS_SOLVER_TYPE_PROJECTION_HIP_RBSOR,
-                                NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI, NS_SOLVER_TYPE_RK4_HIP};
+    const char* hip_names[5] = {NS_SOLVER_TYPE_PROJECTION_HIP, NS_SOLVER_TYPE_PROJECTION_HIP_RBSOR,
+                                NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI, NS_SOLVER_TYPE_RK4_HIP,
+                                NS_SOLVER_TYPE_PROJECTION_HIP_CG1};
     ns_solver_registry_t* reg = cfd_registry_create();
     cfd_registry_register_defaults(reg);
     const char* by_cuda[64];
@@ -51,7 +52,7 @@ int main(void) {
     const char* listed[64];
     const int n_list = simulation_list_solvers(listed, 64);
     int in_cuda = 0, in_list = 0;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
         in_cuda += contains(by_cuda, n_cuda, hip_names[i]);
         in_list += contains(listed, n_list, hip_names[i]);
     }

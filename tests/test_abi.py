@@ -128,7 +128,8 @@ def test_ctypes_layouts_match_c(tmp_path):
 def test_registry_lists_hip_solvers():
     reg = api.Registry()
     names = reg.names()
-    for n in ("projection_hip", "projection_hip_rbsor", "projection_hip_jacobi"):
+    for n in ("projection_hip", "projection_hip_rbsor", "projection_hip_jacobi", "rk4_hip",
+              "projection_hip_cg1"):
         assert n in names
 
 

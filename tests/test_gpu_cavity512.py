@@ -15,6 +15,7 @@ w, p within 1e-9 relative; after steps 1, 6 and 25 the sampled planes
 k = 1, 255, 510 (a stride-4 lattice, rows j = 1, 255, 509, 510, columns
 i = 1, 255, 510) within 1e-9 of the field's largest interior value. The reference's
 own backend-consistency bar is 1e-3 (tests/validation/test_cavity_backends.c:43)."""
+import ctypes as C
 import json
 from pathlib import Path
 
@@ -128,11 +129,13 @@ def test_cavity512_trajectory_vs_oracle(hip_lib):
     print("cavity512 largest deviations from the oracle:", worst)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_cavity512_single_reduction_cg_vs_oracle(hip_lib):
     """The north star's single-reduction CG (cg_variant 1: one reduction per
-    iteration, on one device the fused march k_ccf) on the same trajectory,
-    steps 1-6, against the textbook-CG oracle at the single-device bars
+    iteration, on one device the fused march k_ccf) on the whole 25-step
+    trajectory bench.py times (steps 6-25 after 5 warm-up steps, the 1063 ->
+    1212 iteration jump at step 15 included), against the textbook-CG oracle
+    at the single-device bars, with the sampled planes after steps 1, 6 and 25
     (it is the same Krylov method with other rounding: the iteration counts
     come out identical, profiles/r04_cc_cavity512_vs_oracle.jsonl)."""
     rec = _fixture()
@@ -141,17 +144,70 @@ def test_cavity512_single_reduction_cg_vs_oracle(hip_lib):
     ctx = api.HipProjection(N, N, N, cg_variant=1)
     try:
         _init(ctx)
+        its = []
         worst = {"norm_rel": 0.0, "plane_rel": 0.0}
-        for row in rec["steps"][:6]:
+        for row in rec["steps"]:
             st = A.SolverStats()
             s = ctx.step_device(g, params, st)
             assert s == A.CFD_SUCCESS, (row["step"], s, api._native.last_error())
             ps = ctx.poisson_stats()
+            its.append((ps.iterations, row["cg_iters"]))
             check_step(row, ps.iterations, ps.initial_residual, ps.final_residual,
                        st.max_velocity, st.max_pressure, lambda k: ctx.get_field(FIDS[k]), worst)
     finally:
         ctx.close()
+    assert len(its) == 25
+    print("cavity512 single-reduction CG iterations (device, oracle):", its)
     print("cavity512 single-reduction CG, largest deviations from the oracle:", worst)
+
+
+@pytest.mark.timeout(600)
+def test_cavity512_cg1_plugin_vs_oracle(hip_lib):
+    """The single-reduction CG through the reference interface: the registry
+    name projection_hip_cg1 (cfd_hip_register_solvers, reached by
+    cfd_registry_register_defaults / init_simulation_with_solver,
+    solver_registry.c:213-279) driven by solver_init + solver_step on host
+    buffers, steps 1-2 of the trajectory against the fixture."""
+    rec = _fixture()
+    g = api.Grid(N, N, N, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
+    params = api.validation_params(rec["dt"], 1.0 / rec["re"])
+    f = api.FlowField(N, N, N)
+    for k in ("u", "v", "w", "p", "T"):
+        getattr(f, k)[...] = 0.0
+    f.rho[...] = 1.0
+    api.cavity_bc(f, 1.0)  # the caller BCs once, as the fixture's run
+    reg = api.Registry()
+    solver = reg.create("projection_hip_cg1")
+    try:
+        assert solver.name == "projection_hip_cg1"
+        assert solver.init(g, params) == A.CFD_SUCCESS, api._native.last_error()
+        ctx = solver._ptr.contents.context
+        assert ctx  # the plugin's context exists after init
+        # the plugin keeps the hip_proj context as the first member of its own
+        hctx = C.cast(ctx, C.POINTER(C.c_void_p))[0]
+        lib = api._native.hip()
+        lib.hip_proj_enable_timing(hctx, 1)
+        worst = {"norm_rel": 0.0, "plane_rel": 0.0}
+        for row in rec["steps"][:2]:
+            st = A.SolverStats()
+            s = solver.step(f, g, params, st)
+            assert s == A.CFD_SUCCESS, (row["step"], s, api._native.last_error())
+            assert st.iterations == 1
+            ps = A.PoissonStats()
+            assert lib.hip_proj_get_poisson_stats(hctx, C.byref(ps)) == 0
+            check_step(row, ps.iterations, ps.initial_residual, ps.final_residual,
+                       st.max_velocity, st.max_pressure, lambda k: getattr(f, k), worst)
+        # the fused single-reduction march ran, one launch per CG iteration
+        ms = (C.c_double * 64)()
+        n = (C.c_longlong * 64)()
+        assert lib.hip_proj_get_timing_n(hctx, ms, n, 64) == A.HIP_KT_COUNT
+        total_its = sum(r["cg_iters"] for r in rec["steps"][:2])
+        kt = {k: n[i] for i, k in enumerate(A.KERNEL_TIMERS)}
+        assert abs(kt["cc_fused"] - total_its) <= 2, (kt, total_its)
+        assert kt["cg_sweep_a"] == 0 and kt["cg_sweep_b"] == 0, kt
+    finally:
+        solver.close()
+    print("cavity512 through projection_hip_cg1, largest deviations from the oracle:", worst)
 
 
 @pytest.mark.timeout(900)

@@ -5,8 +5,16 @@ own CMake (CPU only), links libcfd_hip.so by the documented rule and runs
 tests/link/reference_driver.c, a program written against the reference's
 own API (solver_registry.c:213-279,1155-1181,1615-1694;
 simulation_api.c:454-478). Skipped where the reference is absent (the GPU
-box); nothing built from the reference travels there."""
+box); nothing built from the reference travels there.
+
+Opt-in: it configures and compiles the reference tree with the reference's
+OWN build scripts (its CMakeLists.txt, run by cmake in a scratch copy) and
+then runs a program linked against what they built, so it runs only with
+CFD_RUN_REFERENCE_BUILD=1 (`CFD_RUN_REFERENCE_BUILD=1 python -m pytest
+tests/test_reference_build_link.py`). The output of the last such run is
+committed as profiles/r05_reference_link.json."""
 import json
+import os
 import shutil
 import subprocess
 import sys
@@ -16,9 +24,14 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 
-pytestmark = pytest.mark.skipif(not Path("/root/reference/lib/CMakeLists.txt").exists()
-                                or shutil.which("cmake") is None,
-                                reason="the reference tree (or cmake) is not here")
+pytestmark = [
+    pytest.mark.skipif(os.environ.get("CFD_RUN_REFERENCE_BUILD") != "1",
+                       reason="runs the reference's own CMake build: opt in with "
+                              "CFD_RUN_REFERENCE_BUILD=1"),
+    pytest.mark.skipif(not Path("/root/reference/lib/CMakeLists.txt").exists()
+                       or shutil.which("cmake") is None,
+                       reason="the reference tree (or cmake) is not here"),
+]
 
 
 @pytest.fixture(scope="module")
@@ -42,10 +55,11 @@ def test_gpu_symbols_resolve_to_hip_library(linked):
 
 
 def test_registry_lists_the_hip_solvers(linked):
-    """Edits (a), (b), (d): the four names are registered, classified as the
-    GPU backend, and in simulation_list_solvers."""
-    assert linked["hip_names_by_cuda_backend"] == 4
-    assert linked["hip_names_in_simulation_list"] == 4
+    """Edits (a), (b), (d): the five names (projection_hip, _rbsor, _jacobi,
+    rk4_hip, projection_hip_cg1) are registered, classified as the GPU
+    backend, and in simulation_list_solvers."""
+    assert linked["hip_names_by_cuda_backend"] == 5
+    assert linked["hip_names_in_simulation_list"] == 5
 
 
 def test_no_device_here_is_unsupported(linked):

@@ -155,7 +155,8 @@ def test_patched_reference_classifies_hip_as_gpu(host):
     reg = api.Registry()
     lb = host.cfd_registry_list_by_backend
     gpu = _names(lb, reg._ptr, A.NS_SOLVER_BACKEND_CUDA)
-    for n in ("projection_hip", "projection_hip_rbsor", "projection_hip_jacobi", "rk4_hip"):
+    for n in ("projection_hip", "projection_hip_rbsor", "projection_hip_jacobi", "rk4_hip",
+              "projection_hip_cg1"):
         assert n in gpu
         assert n in _names(host.simulation_list_solvers)
     assert lb(reg._ptr, A.NS_SOLVER_BACKEND_SCALAR, None, 0) == 0

@@ -17,7 +17,7 @@ present, so a changed reference fails loudly instead of building unpatched.
   (c) lib/CMakeLists.txt: option CFD_ENABLE_HIP drops the no-CUDA stub from
       cfd_core (:182-185, :247-251) and gives cfd_api CFD_HAS_HIP, our
       include directory and libcfd_hip.so;
-  (d) simulation_api.c s_solver_names (:454-465): the four HIP names.
+  (d) simulation_api.c s_solver_names (:454-465): the five HIP names.
 
 The driver is linked with -rdynamic so that libcfd_hip.so's weak references
 to cfd_registry_register / cfd_set_error bind to the reference's own.
@@ -55,7 +55,8 @@ def patch(src: Path) -> None:
     edit(reg, "    cfd_registry_register(registry, NS_SOLVER_TYPE_RK4_GPU, create_rk4_gpu_solver);\n"
               "#endif\n",
          "#ifdef CFD_HAS_HIP\n"
-         "    /* projection_hip, projection_hip_rbsor, projection_hip_jacobi, rk4_hip */\n"
+         "    /* projection_hip, projection_hip_rbsor, projection_hip_jacobi, rk4_hip,\n"
+         "       projection_hip_cg1 */\n"
          "    cfd_hip_register_solvers(registry);\n#endif\n")
     # (b) backend classification
     edit(reg, '    if (strstr(type_name, "_gpu") != NULL) {\n'
@@ -72,6 +73,7 @@ def patch(src: Path) -> None:
          "#ifdef CFD_HAS_HIP\n"
          "    NS_SOLVER_TYPE_PROJECTION_HIP, NS_SOLVER_TYPE_PROJECTION_HIP_RBSOR,\n"
          "    NS_SOLVER_TYPE_PROJECTION_HIP_JACOBI, NS_SOLVER_TYPE_RK4_HIP,\n"
+         "    NS_SOLVER_TYPE_PROJECTION_HIP_CG1,\n"
          "#endif\n", after=False)
     # (c) CMake: no stub under HIP, and cfd_api gets the library
     cm = src / "lib/CMakeLists.txt"
