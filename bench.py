@@ -102,6 +102,9 @@ def parse():
                          "(Chronopoulos-Gear) CG, one fused z-march per iteration; -1 "
                          "(default): 1 on one GPU at n >= 512, where it is measured faster "
                          "(DESIGN.md section 5), else 0")
+    ap.add_argument("--fixed-cg-iters", type=int, default=200,
+                    help="fixed-iteration CG microbench per variant after the timed region "
+                         "(SURVEY.md §8d config 3; 0: skip)")
     ap.add_argument("--no-compare-cg-variant", action="store_true",
                     help="skip the side measurement of the other CG variant after the "
                          "timed region")
@@ -193,6 +196,7 @@ def main():
 
     if args.cg_variant < 0:
         args.cg_variant = cg_variant_auto(n, world, args.case)
+    solver_name = "projection_hip_cg1" if args.cg_variant == 1 else "projection_hip"
     ctx = make_ctx(args.cg_variant)
 
     def step():
@@ -315,6 +319,23 @@ def main():
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
 
+    # SURVEY.md §8d config 3's fixed-iteration CG microbench (one GPU): 200
+    # iterations, no early exit, x0 = 0, on the last step's own RHS and on
+    # the cos(pi x) cos(pi y) cos(pi z) RHS (interior mean removed), for the
+    # CG variant of this context; the CG-iteration roofline without the
+    # convergence tail or the step's other kernels
+    fixed200 = {}
+    cos_rhs = None
+    if world == 1 and not tg and args.fixed_cg_iters > 0:
+        import numpy as np
+        xs = np.asarray(g.x)
+        cx = np.cos(np.pi * xs)
+        cos_rhs = (cx[:, None, None] * cx[None, :, None]) * cx[None, None, :]
+        cos_rhs -= cos_rhs[1:-1, 1:-1, 1:-1].mean()
+        fixed200[f"cg_variant_{args.cg_variant}"] = fixed_cg(ctx, g, params, n_int,
+                                                             args.cg_variant, cos_rhs,
+                                                             args.fixed_cg_iters)
+
     # side measurement of the other CG variant (same grid, ranks and stepping
     # from the same initial state), after the timed region: per CG iteration,
     # since its iteration counts differ from the main run's by rounding
@@ -345,6 +366,10 @@ def main():
                  "ms_per_cg_iter_wall": round(e2 * 1e3 / max(1, it2), 4),
                  "kernel_ms_per_iter": {k: per2(k) for k in k2 if k2[k][1]},
                  "main_ms_per_cg_iter_wall": round(elapsed * 1e3 / tot_iters, 4)}
+        if cos_rhs is not None:
+            fixed200[f"cg_variant_{1 - args.cg_variant}"] = fixed_cg(
+                ctx, g, params, n_int, 1 - args.cg_variant, cos_rhs, args.fixed_cg_iters)
+    del cos_rhs
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
@@ -367,7 +392,12 @@ def main():
                      else "synthetic (cavity at rest + lid BC, generated in HBM)"),
             "config": {"workload": (f"{n}^3 Taylor-Green nu=0.01, dt=1e-3" if tg else
                                     f"{n}^3 lid-driven cavity Re={args.re:g}, dt={args.dt:g}")
-                                   + ", projection_hip (CG rel 1e-6)",
+                                   + f", {solver_name} (CG rel 1e-6"
+                                   + (", single-reduction Chronopoulos-Gear CG)"
+                                      if args.cg_variant == 1 else ", textbook CG)"),
+                       # the registry name whose pressure solve this run times
+                       # (projection_hip_plugin.c cfd_hip_register_solvers)
+                       "solver": solver_name,
                        "grid": [n, n, n], "interior_cells": n_int,
                        "parallelism": (f"z-slab x{world} (RCCL halo, "
                                        + ("peer-memory" if comm.device_allreduce else "RCCL")
@@ -402,6 +432,8 @@ def main():
             "ranks": ranks,
             "cg_variant": args.cg_variant,
             "cg_variant_compare": other,
+            "cg_fixed200": ({"iterations": args.fixed_cg_iters, "x0": "zero",
+                             "early_exit": False, **fixed200} if fixed200 else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
@@ -631,6 +663,32 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
             ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, {rev}>", BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))
+
+
+BYTES_CG_TEXTBOOK = 58.0  # textbook CG per iteration: sweeps A + B (48) + the x fold / 4 (10)
+
+
+def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
+    """ms per iteration of `iters` CG iterations (no early exit, x0 = 0) on the
+    context's last step's RHS and on cos_rhs, with the algorithmic rate in
+    both byte models (42 B/cell: the single-reduction march; 58: textbook)."""
+    rho_over_dt = 1.0 / params.dt  # rho = 1 (the cavity)
+    out = {"bytes_per_cell_moved": BYTES_CC_FUSED if cg_variant == 1 else BYTES_CG_TEXTBOOK}
+    for name, rhs in (("step_rhs", None), ("cos_rhs", cos_rhs)):
+        if rhs is None:
+            ms = ctx.cg_fixed_iters_step_rhs(g.dx, g.dy, g.dz, iters, rho_over_dt)
+        else:
+            ms = ctx.cg_fixed_iters(rhs, g.dx, g.dy, g.dz, iters)
+        if ms <= 0:
+            out[name] = None
+            continue
+        per = ms / iters
+        out[name] = {"ms_per_iter": round(per, 4),
+                     "GBps_42": round(BYTES_CC_FUSED * n_int / (per * 1e-3) / 1e9, 1),
+                     "GBps_58": round(BYTES_CG_TEXTBOOK * n_int / (per * 1e-3) / 1e9, 1),
+                     "frac_of_8TBps_own_bytes": round(out["bytes_per_cell_moved"] * n_int
+                                                      / (per * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    return out
 
 
 def cg_variant_auto(n, world, case="cavity"):

@@ -198,6 +198,8 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_row_pitch", C.c_size_t, V)
     _sig(lib, "hip_proj_cg_fixed_iters", C.c_double, V, A.c_double_p, C.c_double, C.c_double,
          C.c_double, C.c_int)
+    _sig(lib, "hip_proj_cg_fixed_iters_ex", C.c_double, V, A.c_double_p, C.c_double,
+         C.c_double, C.c_double, C.c_int, C.c_double)
     _sig(lib, "hip_proj_poisson_solve", C.c_int, V, C.c_int, A.c_double_p, A.c_double_p,
          C.c_double, C.c_double, C.c_double, P(A.PoissonParams), P(A.PoissonStats))
     _sig(lib, "hip_proj_poisson_solve_ex", C.c_int, V, C.c_int, A.c_double_p, A.c_double_p,

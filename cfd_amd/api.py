@@ -606,6 +606,11 @@ class HipProjection:
         return self._lib().hip_proj_cg_fixed_iters(self._ctx, a.ctypes.data_as(A.c_double_p),
                                                    dx, dy, dz, iters)
 
+    def cg_fixed_iters_step_rhs(self, dx, dy, dz, iters: int, rho_over_dt: float) -> float:
+        """hip_proj_cg_fixed_iters_ex with the last step's RHS (rho/dt) div u*."""
+        return self._lib().hip_proj_cg_fixed_iters_ex(self._ctx, None, dx, dy, dz, iters,
+                                                      rho_over_dt)
+
     def close(self):
         if getattr(self, "_ctx", None):
             _native.hip().hip_proj_destroy(self._ctx)

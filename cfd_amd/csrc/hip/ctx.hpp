@@ -127,7 +127,11 @@ struct hip_proj_ctx {
     double* rk_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // RK4 k1 + 2k2 + 2k3
     double *dxa = nullptr, *dya = nullptr;  // grid->dx[], grid->dy[] (RK4 per-index spacing)
     double *src_u_row = nullptr, *src_v_col = nullptr;
-    std::vector<double> h_src_u, h_src_v;
+    // pinned host staging of the source-term tables (ny rows, then nx columns):
+    // a plain DMA each step, never a staged pageable copy; ev_src marks the
+    // last upload, so the host rewrites the tables only after it landed
+    double* h_src = nullptr;
+    hipEvent_t ev_src = nullptr;
     // reductions / state
     CgState* st = nullptr;
     RxState* rxst = nullptr;             // fused relaxation loop state
@@ -337,6 +341,52 @@ static const unsigned long long* reduce_red(hip_proj_ctx* c, cfd_status_t* st) {
         cfd_status_t s_ = (expr);               \
         if (s_ != CFD_SUCCESS) return s_;       \
     } while (0)
+
+// compute_source_terms at `iter` (solver_explicit_euler.c:317-333) on the
+// host with the reference's libm expressions, uploaded to src_u_row /
+// src_v_col from the pinned staging
+static cfd_status_t upload_source_tables(hip_proj_ctx* c, const grid* g,
+                                         const ns_solver_params_t* prm, int iter) {
+    const size_t nx = c->nx, ny = c->ny;
+    const double dt = prm->dt;
+    HIP_TRY(hipEventSynchronize(c->ev_src));
+    double* hu = c->h_src;
+    double* hv = c->h_src + ny;
+    for (size_t j = 0; j < ny; j++)
+        hu[j] = prm->source_amplitude_u * sin(M_PI * g->y[j]) *
+                exp(-prm->source_decay_rate * iter * dt);
+    for (size_t i = 0; i < nx; i++)
+        hv[i] = prm->source_amplitude_v * sin(2.0 * M_PI * g->x[i]) *
+                exp(-prm->source_decay_rate * iter * dt);
+    HIP_TRY(hipMemcpyAsync(c->src_u_row, hu, ny * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipMemcpyAsync(c->src_v_col, hv, nx * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipEventRecord(c->ev_src, c->stream));
+    return CFD_SUCCESS;
+}
+
+// In-process Z-slab groups (slab_comm.hip LocalComm) drive their ranks'
+// contexts from several host threads of one process. Their host work is
+// serialised: a hip_proj_* entry point on a group context holds the group's
+// host lock for the whole call, and a rank gives it up only while it waits
+// at a group barrier (hip_proj_group::barrier). The device work of the ranks
+// still overlaps (each rank has its own streams); what can no longer happen
+// is two rank threads inside the HIP runtime or this library at once
+// (the intermittent host segfault of the 3-rank Jacobi test).
+// RCCL contexts (one process per GPU) and single-device contexts: no lock.
+void group_host_enter(hip_proj_group* g) __attribute__((visibility("hidden")));
+void group_host_leave(hip_proj_group* g) __attribute__((visibility("hidden")));
+struct GroupHostLock {
+    hip_proj_group* g;
+    explicit GroupHostLock(const hip_proj_ctx* c)
+        : g((c && c->comm) ? c->comm->host_group() : nullptr) {
+        group_host_enter(g);
+    }
+    ~GroupHostLock() { group_host_leave(g); }
+    GroupHostLock(const GroupHostLock&) = delete;
+    GroupHostLock& operator=(const GroupHostLock&) = delete;
+};
 
 
 // Shared by the integrators (defined in projection_hip.hip).

@@ -1147,6 +1147,8 @@ static void free_ctx(hip_proj_ctx* c) {
     if (c->dsum) hipFree(c->dsum);
     if (c->h_state) hipHostFree(c->h_state);
     if (c->h_red) hipHostFree(c->h_red);
+    if (c->h_src) hipHostFree(c->h_src);
+    if (c->ev_src) hipEventDestroy(c->ev_src);
     if (c->shell_host) hipHostFree(c->shell_host);
     if (c->shell_dev) hipFree(c->shell_dev);
     for (int i = 0; i < 2; i++)
@@ -1470,6 +1472,8 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     }
     if (dalloc(c, &c->src_u_row, ny) != CFD_SUCCESS) return CFD_ERROR;
     if (dalloc(c, &c->src_v_col, nx) != CFD_SUCCESS) return CFD_ERROR;
+    HIP_TRY(hipHostMalloc((void**)&c->h_src, (nx + ny) * sizeof(double), hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_src, hipEventDisableTiming));
     HIP_TRY(hipMalloc((void**)&c->st, sizeof(CgState)));
     HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
     // x2: the single-reduction CG reduces two values per workgroup
@@ -1579,6 +1583,7 @@ size_t hip_proj_device_bytes(const hip_proj_ctx_t* ctx) { return ctx ? ctx->byte
 size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx) { return ctx ? (size_t)ctx->px : 0; }
 
 cfd_status_t hip_proj_synchronize(hip_proj_ctx_t* c) {
+    GroupHostLock hl_(c);
     if (!c) return CFD_ERROR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1587,6 +1592,7 @@ cfd_status_t hip_proj_synchronize(hip_proj_ctx_t* c) {
 }
 
 cfd_status_t hip_proj_set_field(hip_proj_ctx_t* c, int id, const double* host) {
+    GroupHostLock hl_(c);
     if (!c || !host) return CFD_ERROR_INVALID;
     double* d = field_ptr(c, id);
     if ((id == HIP_FIELD_T || id == HIP_FIELD_RHO) && !d) {
@@ -1606,6 +1612,7 @@ cfd_status_t hip_proj_set_field(hip_proj_ctx_t* c, int id, const double* host) {
 }
 
 cfd_status_t hip_proj_get_field(hip_proj_ctx_t* c, int id, double* host) {
+    GroupHostLock hl_(c);
     if (!c || !host) return CFD_ERROR_INVALID;
     double* d = field_ptr(c, id);
     if (!d) return CFD_ERROR_INVALID;
@@ -1624,6 +1631,7 @@ static __global__ void k_fill(double* f, long long n, double v) {
 }
 
 cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
+    GroupHostLock hl_(c);
     if (!c) return CFD_ERROR_INVALID;
     double* d = field_ptr(c, id);
     if ((id == HIP_FIELD_T || id == HIP_FIELD_RHO) && !d) {
@@ -1643,6 +1651,7 @@ cfd_status_t hip_proj_fill_field(hip_proj_ctx_t* c, int id, double value) {
 }
 
 cfd_status_t hip_proj_set_density(hip_proj_ctx_t* c, double rho0) {
+    GroupHostLock hl_(c);
     if (!c) return CFD_ERROR_INVALID;
     c->rho0 = rho0;
     // a per-cell density array (RK4, restart files) follows the uniform value
@@ -1651,6 +1660,7 @@ cfd_status_t hip_proj_set_density(hip_proj_ctx_t* c, double rho0) {
 }
 
 cfd_status_t hip_proj_upload(hip_proj_ctx_t* c, const flow_field* f) {
+    GroupHostLock hl_(c);
     if (!c || !f) return CFD_ERROR_INVALID;
     if (f->nx != c->nx || f->ny != c->ny || f->nz != c->nz) return CFD_ERROR_INVALID;
     cfd_status_t s;
@@ -1671,6 +1681,7 @@ cfd_status_t hip_proj_upload(hip_proj_ctx_t* c, const flow_field* f) {
 }
 
 cfd_status_t hip_proj_download(hip_proj_ctx_t* c, flow_field* f) {
+    GroupHostLock hl_(c);
     if (!c || !f) return CFD_ERROR_INVALID;
     cfd_status_t s;
     if ((s = hip_proj_get_field(c, HIP_FIELD_U, f->u)) != CFD_SUCCESS) return s;
@@ -1681,6 +1692,7 @@ cfd_status_t hip_proj_download(hip_proj_ctx_t* c, flow_field* f) {
 }
 
 cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type) {
+    GroupHostLock hl_(c);
     if (!c) return CFD_ERROR_INVALID;
     c->resident = 0;
     double* d = field_ptr(c, id);
@@ -1709,6 +1721,7 @@ cfd_status_t hip_proj_apply_scalar_bc(hip_proj_ctx_t* c, int id, bc_type_t type)
 }
 
 cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* c, int id, const bc_dirichlet_values_t* v) {
+    GroupHostLock hl_(c);
     if (!c || !v) return CFD_ERROR_INVALID;
     c->resident = 0;
     double* d = field_ptr(c, id);
@@ -1721,6 +1734,7 @@ cfd_status_t hip_proj_apply_dirichlet(hip_proj_ctx_t* c, int id, const bc_dirich
 }
 
 cfd_status_t hip_proj_apply_thermal_bcs(hip_proj_ctx_t* c, const ns_solver_params_t* prm) {
+    GroupHostLock hl_(c);
     if (!c || !prm) return CFD_ERROR_INVALID;
     c->resident = 0;
     if (!c->T) {
@@ -1735,16 +1749,19 @@ cfd_status_t hip_proj_apply_thermal_bcs(hip_proj_ctx_t* c, const ns_solver_param
 }
 
 cfd_status_t hip_proj_get_poisson_stats(hip_proj_ctx_t* c, poisson_solver_stats_t* s) {
+    GroupHostLock hl_(c);
     if (!c || !s) return CFD_ERROR_INVALID;
     *s = c->pstats;
     return CFD_SUCCESS;
 }
 
 void hip_proj_enable_timing(hip_proj_ctx_t* c, int enable) {
+    GroupHostLock hl_(c);
     if (c) c->timing = enable ? 1 : 0;
 }
 
 void hip_proj_reset_timing(hip_proj_ctx_t* c) {
+    GroupHostLock hl_(c);
     if (!c) return;
     hipStreamSynchronize(c->stream);
     flush_timing(c);
@@ -1756,6 +1773,7 @@ void hip_proj_reset_timing(hip_proj_ctx_t* c) {
 
 int hip_proj_get_timing_n(hip_proj_ctx_t* c, double* total_ms, long long* launches,
                           int capacity) {
+    GroupHostLock hl_(c);
     if (!c || capacity <= 0) return 0;
     hipStreamSynchronize(c->stream);
     flush_timing(c);
@@ -1865,18 +1883,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     }
 
     // source-term tables: compute_source_terms at iter = 0 (solver_explicit_euler.c:317-333)
-    c->h_src_u.resize(ny);
-    c->h_src_v.resize(nx);
-    for (size_t j = 0; j < ny; j++)
-        c->h_src_u[j] = prm->source_amplitude_u * sin(M_PI * g->y[j]) *
-                        exp(-prm->source_decay_rate * iter * dt);
-    for (size_t i = 0; i < nx; i++)
-        c->h_src_v[i] = prm->source_amplitude_v * sin(2.0 * M_PI * g->x[i]) *
-                        exp(-prm->source_decay_rate * iter * dt);
-    HIP_TRY(hipMemcpyAsync(c->src_u_row, c->h_src_u.data(), ny * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->src_v_col, c->h_src_v.data(), nx * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
+    ST_TRY(upload_source_tables(c, g, prm, iter));
 
     PredCoef2 pc;
     pc.two_dx = 2.0 * dx;
@@ -2027,6 +2034,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
 }
 
 cfd_status_t hip_proj_mark_host_dirty(hip_proj_ctx_t* c) {
+    GroupHostLock hl_(c);
     if (!c) return CFD_ERROR_INVALID;
     c->resident = 0;
     c->hash_ok = 0;
@@ -2035,6 +2043,7 @@ cfd_status_t hip_proj_mark_host_dirty(hip_proj_ctx_t* c) {
 
 cfd_status_t hip_proj_step_device(hip_proj_ctx_t* c, const grid* g,
                                   const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
+    GroupHostLock hl_(c);
     if (c) c->resident = 0;
     return step_device_impl(c, g, prm, stats, 0);
 }
@@ -2198,10 +2207,12 @@ extern "C" {
 
 cfd_status_t hip_proj_step(hip_proj_ctx_t* c, flow_field* f, const grid* g,
                            const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
+    GroupHostLock hl_(c);
     return host_steps(c, f, g, prm, stats, 1, true);
 }
 
 cfd_status_t hip_proj_sync_host(hip_proj_ctx_t* c, flow_field* f) {
+    GroupHostLock hl_(c);
     if (!c || !f) return CFD_ERROR_INVALID;
     if (f->nx != c->nx || f->ny != c->ny || f->nz != c->nz) return CFD_ERROR_INVALID;
     ST_TRY(hip_proj_download(c, f));
@@ -2224,6 +2235,7 @@ cfd_status_t hip_proj_poisson_solve(hip_proj_ctx_t* c, int method, double* x, co
                                     double dx, double dy, double dz,
                                     const poisson_solver_params_t* params,
                                     poisson_solver_stats_t* stats) {
+    GroupHostLock hl_(c);
     return hip_proj_poisson_solve_ex(c, method, x, rhs, dx, dy, dz, params, stats,
                                      HIP_POISSON_BC_NEUMANN, nullptr);
 }
@@ -2238,6 +2250,7 @@ cfd_status_t hip_proj_poisson_solve_ex(hip_proj_ctx_t* c, int method, double* x,
                                        const poisson_solver_params_t* params,
                                        poisson_solver_stats_t* stats, int bc_mode,
                                        const double* bc_values) {
+    GroupHostLock hl_(c);
     if (c) c->resident = 0;  // the solve reuses the step's pressure buffers
     if (!c || !x || !rhs) return CFD_ERROR_INVALID;
     if (bc_mode != HIP_POISSON_BC_NEUMANN && bc_mode != HIP_POISSON_BC_NONE &&
@@ -2308,21 +2321,39 @@ static cfd_status_t poisson_solve_impl(hip_proj_ctx_t* c, int method, double* x,
 
 double hip_proj_cg_fixed_iters(hip_proj_ctx_t* c, const double* rhs_host, double dx, double dy,
                                double dz, int iters) {
-    if (!c || !rhs_host || iters <= 0) return -1.0;
+    if (!rhs_host) return -1.0;
+    return hip_proj_cg_fixed_iters_ex(c, rhs_host, dx, dy, dz, iters, 0.0);
+}
+
+double hip_proj_cg_fixed_iters_ex(hip_proj_ctx_t* c, const double* rhs_host, double dx,
+                                  double dy, double dz, int iters, double rho_over_dt) {
+    GroupHostLock hl_(c);
+    if (!c || iters <= 0) return -1.0;
     if (hipSetDevice(c->device) != hipSuccess) return -1.0;
-    if (ensure_aux(c, true, false) != CFD_SUCCESS) return -1.0;
-    if (hipMemcpy2DAsync(c->rhs, c->px * sizeof(double), rhs_host, c->nx * sizeof(double),
-                         c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
-                         c->stream) != hipSuccess)
-        return -1.0;
+    if (!rhs_host && (!c->us || !c->vs || !c->ws)) return -1.0;
+    if (rhs_host) {
+        if (ensure_aux(c, true, false) != CFD_SUCCESS) return -1.0;
+        if (hipMemcpy2DAsync(c->rhs, c->px * sizeof(double), rhs_host, c->nx * sizeof(double),
+                             c->nx * sizeof(double), c->ny * c->nz, hipMemcpyHostToDevice,
+                             c->stream) != hipSuccess)
+            return -1.0;
+    }
     hipMemsetAsync(c->pn, 0, field_elems(c) * sizeof(double), c->stream);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
+    // rhs_host == NULL: the step's own right-hand side, (rho/dt) div u* of the
+    // context's u*, v*, w* (the last step's predictor output), fused into the
+    // CG setup exactly as the step forms it
     DivCoef dc{};
+    dc.two_dx = 2.0 * dx;
+    dc.two_dy = 2.0 * dy;
+    dc.inv_2dz = (c->nzg > 1 && dz > 0.0) ? 1.0 / (2.0 * dz) : 0.0;
+    dc.rho_over_dt = rho_over_dt;
     hipEventRecord(a, c->stream);
     // zero tolerances: no early exit, exactly `iters` iterations
-    cfd_status_t s = cg_solve(c, dx, dy, dz, dc, RHS_FROM_ARRAY, 0.0, 0.0, iters, 1, false);
+    cfd_status_t s = cg_solve(c, dx, dy, dz, dc, rhs_host ? RHS_FROM_ARRAY : RHS_FROM_VELOCITY,
+                              0.0, 0.0, iters, 1, false);
     (void)s;
     hipEventRecord(b, c->stream);
     hipEventSynchronize(b);

@@ -85,18 +85,7 @@ static cfd_status_t rk4_step_impl(hip_proj_ctx* c, const grid* g, const ns_solve
     // evaluated on the host with the reference's libm expressions
     HIP_TRY(hipMemcpyAsync(c->dxa, g->dx, nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->dya, g->dy, ny * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    c->h_src_u.resize(ny);
-    c->h_src_v.resize(nx);
-    for (size_t j = 0; j < ny; j++)
-        c->h_src_u[j] = prm->source_amplitude_u * sin(M_PI * g->y[j]) *
-                        exp(-prm->source_decay_rate * iter * dt);
-    for (size_t i = 0; i < nx; i++)
-        c->h_src_v[i] = prm->source_amplitude_v * sin(2.0 * M_PI * g->x[i]) *
-                        exp(-prm->source_decay_rate * iter * dt);
-    HIP_TRY(hipMemcpyAsync(c->src_u_row, c->h_src_u.data(), ny * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->src_v_col, c->h_src_v.data(), nx * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
+    ST_TRY(upload_source_tables(c, g, prm, iter));
 
     RkCoef rc;
     rc.inv_2dz = (nz > 1 && g->dz) ? 1.0 / (2.0 * g->dz[0]) : 0.0;
@@ -195,11 +184,13 @@ extern "C" {
 
 cfd_status_t hip_rk4_step_device(hip_proj_ctx_t* c, const grid* g, const ns_solver_params_t* prm,
                                  ns_solver_stats_t* stats) {
+    GroupHostLock hl_(c);
     return rk4_step_impl(c, g, prm, stats, 0);
 }
 
 cfd_status_t hip_rk4_step(hip_proj_ctx_t* c, flow_field* f, const grid* g,
                           const ns_solver_params_t* prm, ns_solver_stats_t* stats) {
+    GroupHostLock hl_(c);
     return hip_rk4_step_iter_internal(c, f, g, prm, stats, 1);
 }
 

@@ -237,8 +237,15 @@ __global__ void k_group_max_u64(GroupPtrs in, unsigned long long* out, int count
 
 }  // namespace
 
+struct hip_proj_group;
+// the group whose host lock this thread holds, and the entry-point nesting
+// depth (an entry point may call another: only the outermost locks)
+static thread_local hip_proj_group* t_held = nullptr;
+static thread_local int t_depth = 0;
+
 struct hip_proj_group {
     int size = 0;
+    std::mutex host;  // serialises the ranks' host work (ctx.hpp GroupHostLock)
     std::mutex m;
     std::condition_variable cv;
     int arrived = 0;
@@ -252,7 +259,18 @@ struct hip_proj_group {
 
     // false once any rank timed out: a rank that failed before reaching a
     // collective must not leave the others blocked forever.
+    // The host lock is given up while waiting (the other ranks must reach
+    // the barrier) and taken back before returning.
     bool barrier() {
+        const bool held = (t_held == this);
+        if (held) host.unlock();
+        const bool ok = wait_all_ranks();
+        if (held) host.lock();
+        return ok;
+    }
+
+  private:
+    bool wait_all_ranks() {
         std::unique_lock<std::mutex> lk(m);
         if (broken) return false;
         const unsigned long long my = gen;
@@ -273,10 +291,27 @@ struct hip_proj_group {
     }
 };
 
+__attribute__((visibility("hidden"))) void group_host_enter(hip_proj_group* g) {
+    if (!g) return;
+    if (t_depth++ == 0) {
+        g->host.lock();
+        t_held = g;
+    }
+}
+
+__attribute__((visibility("hidden"))) void group_host_leave(hip_proj_group* g) {
+    if (!g) return;
+    if (--t_depth == 0) {
+        t_held = nullptr;
+        g->host.unlock();
+    }
+}
+
 namespace {
 
 struct LocalComm final : SlabComm {
     hip_proj_group* G = nullptr;
+    hip_proj_group* host_group() override { return G; }
 
     cfd_status_t meet() {
         if (!G->barrier()) return fail(CFD_ERROR, "in-process group barrier timed out", nullptr);

@@ -20,6 +20,7 @@
 namespace cfdhip {
 struct Mbox;
 }
+struct hip_proj_group;
 
 struct SlabComm {
     int rank = 0, size = 1, device = 0;
@@ -37,6 +38,9 @@ struct SlabComm {
     // Device mailbox for the one-shot CG dot all-reduce fused into the sweeps
     // (kernels.hpp mbox_allreduce); nullptr = all-reduce through allreduce_sum.
     virtual cfdhip::Mbox* device_mailbox() { return nullptr; }
+    // the in-process group whose host lock this rank's calls take (ctx.hpp
+    // GroupHostLock); nullptr for RCCL
+    virtual hip_proj_group* host_group() { return nullptr; }
 };
 
 struct hip_proj_comm {

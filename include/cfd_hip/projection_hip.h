@@ -256,6 +256,14 @@ CFD_HIP_EXPORT size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx);
  * iterations with no early exit. Returns elapsed device ms (events). */
 CFD_HIP_EXPORT double hip_proj_cg_fixed_iters(hip_proj_ctx_t* ctx, const double* rhs_host,
                                               double dx, double dy, double dz, int iters);
+/* The same with the right-hand side of the most recent step: rhs_host == NULL
+ * solves with rhs = rho_over_dt * div u* of the context's predictor output
+ * (the RHS the step's CG setup forms, solver_projection.c:195-214), x0 = 0;
+ * rhs_host != NULL is hip_proj_cg_fixed_iters. The context's cg_variant
+ * selects the CG form. SURVEY.md §8d config 3's fixed-200-iteration run. */
+CFD_HIP_EXPORT double hip_proj_cg_fixed_iters_ex(hip_proj_ctx_t* ctx, const double* rhs_host,
+                                                 double dx, double dy, double dz, int iters,
+                                                 double rho_over_dt);
 
 /* Restart files of the device-resident state, in the reference's .cfdchk
  * format (cfd_checkpoint_write / cfd_checkpoint_read, lib/include/cfd/io/

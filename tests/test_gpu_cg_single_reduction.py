@@ -101,10 +101,20 @@ def test_trivial_and_capped(hip_lib):
         ctx.close()
 
 
-@pytest.mark.parametrize("nranks", [2, 4])
-def test_slab_poisson_matches_single_device(hip_lib, nranks):
-    g, rhs = cases.cos_rhs(33)
-    ctx = api.HipProjection(33, 33, 33, **CC)
+@pytest.mark.parametrize("nranks,n", [(2, 33), (4, 33), (4, 13), (8, 17), (4, 9)])
+def test_slab_poisson_matches_single_device(hip_lib, nranks, n):
+    """33^3: every slab >= 3 planes (the edge-plane launch, the r halo on the
+    side stream over the interior launch); 13^3 on 4 ranks mixes 3- and
+    2-plane slabs, 17^3 on 8 ranks 2- and 1-plane ones, 9^3 on 4 ranks 2 and
+    1: slabs of < 3 planes run the whole march, then a blocking r halo
+    (projection_hip.hip iterate_cc), beside neighbours that split."""
+    spans = [api.slab_layout(n, r, nranks)[1] - 2 for r in range(nranks)]
+    if n == 13:
+        assert sorted(set(spans)) == [2, 3]
+    elif n != 33:
+        assert min(spans) < 3
+    g, rhs = cases.cos_rhs(n)
+    ctx = api.HipProjection(n, n, n, **CC)
     try:
         x1 = np.zeros_like(rhs)
         s1, st1 = ctx.poisson_solve(A.HIP_POISSON_CG, x1, rhs, g.dx, g.dy, g.dz)

@@ -331,3 +331,56 @@ def test_slab8_cavity_rbsor_depth_bitwise(hip_lib, omp_oracle, monkeypatch, spli
     assert all(it > 10 for it, _, _ in ohist)
     for k in FIELDS:
         np.testing.assert_array_equal(got[k], getattr(f, k), err_msg=k)
+
+
+@pytest.mark.timeout(600)
+def test_slab8_taylor_green_512_vs_single_device(hip_lib, monkeypatch):
+    """BASELINE configs[3] at its own size: 512^3 Taylor-Green on 8
+    in-process Z-slabs (6 x 64 + 2 x 63 interior planes, the periodic z wrap
+    as the exchange between ranks 0 and 7) against one context on the same
+    device, 2 steps with the periodic BCs before each step
+    (taylor_green_3d_reference.h:177-404). Gates:
+    identical CG iteration counts, the relative L2 errors of u and v against
+    the analytic decay equal within 1e-10 relative, and the fields within
+    1e-10 of their scale."""
+    monkeypatch.setenv("CFD_HIP_GROUP_TIMEOUT_S", "120")
+    n, steps = 512, 2
+    g, f, p = cases.tg3(n)
+    one = api.HipProjection(n, n, n)
+    try:
+        for k, fid in FIELDS.items():
+            one.set_field(fid, getattr(f, k))
+        one.set_density(1.0)
+        its1 = []
+        for _ in range(steps):
+            _tg_bc_device(one)
+            assert one.step_device(g, p) == A.CFD_SUCCESS, api._native.last_error()
+            its1.append(one.poisson_stats().iterations)
+        ref = {k: one.get_field(fid) for k, fid in FIELDS.items()}
+    finally:
+        one.close()
+    S = Slabs(g, 8)
+    try:
+        assert [c.nz_local - 2 for c in S.ctx] == [64] * 6 + [63] * 2
+        S.scatter(f)
+        hist = _run_steps(S, g, p, steps, _tg_bc_device)
+        got = {k: S.gather(k) for k in FIELDS}
+    finally:
+        S.close()
+    for r in range(8):
+        assert [h[0] for h in hist[r]] == its1, (r, hist[r], its1)
+    assert all(i > 100 for i in its1)
+    t = steps * p.dt
+    for k in FIELDS:
+        f_k = getattr(f, k)
+        f_k[...] = ref[k]
+    e1 = cases.tg3_l2_errors(g, f, t)
+    for k in FIELDS:
+        getattr(f, k)[...] = got[k]
+    eN = cases.tg3_l2_errors(g, f, t)
+    for a, b in zip(e1, eN):
+        assert b == pytest.approx(a, rel=1e-10), (e1, eN)
+    for k in FIELDS:
+        scale = max(1.0, float(np.max(np.abs(ref[k]))))
+        assert float(np.max(np.abs(got[k] - ref[k]))) / scale <= 1e-10, k
+    print("tg512 on 8 slabs: CG iterations", its1, "L2 errors (1 device, 8 slabs)", e1, eN)
