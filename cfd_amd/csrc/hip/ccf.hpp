@@ -35,6 +35,13 @@
 
 namespace cfdhip {
 
+// planes of r_it, p_{it-1} in flight ahead of their use (1 or 2; the
+// build's -DCFD_CCF_AHEAD selects it for A/B runs)
+#ifndef CFD_CCF_AHEAD
+#define CFD_CCF_AHEAD 2
+#endif
+constexpr int CCF_AHEAD = CFD_CCF_AHEAD;
+static_assert(CCF_AHEAD == 1 || CCF_AHEAD == 2, "k_ccf prefetch depth");
 constexpr int CCF_TC = 32;  // x pairs per tile row
 constexpr int CCF_TR = 32;  // tile rows
 constexpr int CCF_OX = 60;  // columns written per tile
@@ -142,9 +149,25 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     for (int s = 0; s < 4; ++s) pn[s] = rn[s] = po[s] = rr[s] = zero;
     fx[0] = fx[1] = f0[0] = f0[1] = f1[0] = f1[1] = f2[0] = f2[1] = zero;
     // (r_it of plane q0 + 1 = kb - 3 only feeds r_{it+1} there, never used)
-    rr[2] = ld2(R0, plane(q0 + 2) + col);
-    if (!FIRST) po[2] = ld2(Po, plane(q0 + 2) + col);
     // (the fold operands of plane q0 + 1 = kb - 3 are never stored: no load)
+    // Each prologue load is followed by dropped stores in the place of a
+    // step's stores, so that the first steps' waits for these loads count the
+    // same ops as every later step's (the loop header joins both paths).
+    auto pro = [&](int k) __attribute__((always_inline)) {
+        const int s = (k - q0) & 3;
+        rr[s] = ld2b(R0 + plane(k), g.ps, col * 8);
+        if (!FIRST) po[s] = ld2b(Po + plane(k), g.ps, col * 8);
+        st2b<false>(Pn, g.ps, ST_NOSTORE, zero);
+        st2b<false>(R1, g.ps, ST_NOSTORE, zero);
+        if (FOLD) st2b<false>(x, g.ps, ST_NOSTORE, zero);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // AHEAD 1: plane q0 + 2 here, step q loads q + 3; AHEAD 2: planes q0 + 2
+    // and q0 + 3 here, step q loads q + 4 (into the slot of plane q, which no
+    // step from q on reads: stage a reads q + 2, stage b q + 1)
+    rr[2] = po[2] = zero;
+    pro(q0 + 2);
+    if (CCF_AHEAD == 2) pro(q0 + 3);
     double accg = 0.0, accd = 0.0;
     auto step = [&](auto Pc, int q) __attribute__((always_inline)) {
         constexpr int P = decltype(Pc)::value;
@@ -153,25 +176,43 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         constexpr int F1 = (P + 1) & 1, F2 = P & 1;  // fold slots of planes q + 1, q + 2
         constexpr int LPR = (P + 1) & 1, LPW = P & 1;        // p_it planes q + 1 (read), q + 2
         constexpr int LRR = 2 + (P & 1), LRW = 2 + ((P + 1) & 1);  // r_{it+1} q (read), q + 1
-        // prefetch plane q + 3 (r_it, p_{it-1}) and the fold operands of q + 2
-        // (two steps ahead measured slower: 1.32 vs 1.27 ms per iteration at
-        // 512^3, profiles/r04_ccf_prefetch2_cg_variant.jsonl)
-        if (q + 1 < ke) {  // the last step has no next step to load for
-            // (skipping the two unused edge-plane loads: 1.157 -> 1.119 ms per
-            // iteration at 512^3, profiles/r04_ccf_edge_plane_loads_ab.jsonl)
-            rr[S3] = ld2(R0, plane(q + 3) + col);
-            if (!FIRST) po[S3] = ld2(Po, plane(q + 3) + col);
+        // prefetch plane q + 2 + AHEAD (r_it, p_{it-1}) and the fold operands
+        // of q + 2 (r04, with the branch-conservative waits below: two steps
+        // ahead measured slower, 1.32 vs 1.27 ms per iteration at 512^3,
+        // profiles/r04_ccf_prefetch2_cg_variant.jsonl)
+        // Memory ops of a step in a fixed order with no branch around any of
+        // them: the loads of plane q + 2 + AHEAD (r_it, p_{it-1}) and the fold
+        // operands of plane q + 2 first, then (end of the step) the stores of
+        // plane q + 1. With every step issuing the same ops the compiler's
+        // vmcnt count is exact, and the wait before the next barrier (for
+        // these loads) leaves the stores issued after them in flight; a load
+        // or store under a branch makes the count at the join conservative,
+        // and that wait then also waits for the stores just issued.
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            // plane q + AHEAD + 2; the planes past ke + 1 (the last steps')
+            // no step reads: those loads are dropped (offset past the plane:
+            // no memory access; the unused edge-plane reads cost 1.157 vs 1.119
+            // ms per iteration at 512^3, profiles/r04_ccf_edge_plane_loads_ab.jsonl)
+            constexpr int SL = (CCF_AHEAD == 2) ? S0 : S3;
+            const int ql = q + CCF_AHEAD + 2;
+            const long long pbl = plane(ql);
+            const int ol = (ql <= ke + 1) ? col * 8 : ST_NOSTORE;
+            rr[SL] = ld2b(R0 + pbl, g.ps, ol);
+            if (!FIRST) po[SL] = ld2b(Po + pbl, g.ps, ol);
         }
-        if (FOLD && wr && q + 2 >= kb && q + 2 < ke) {
+        if (FOLD) {
             // only the lanes and planes that store x read its operands (the
             // halo lanes' and planes' loads would be re-fetched lines): 1.123
             // vs 1.159 ms per iteration at 512^3, profiles/r04_ccf_fold_owned_loads_ab.jsonl
-            const long long o = plane(q + 2) + col;
-            fx[F2] = ld2(x, o);
-            f0[F2] = ld2(pv.q[0], o);
-            f1[F2] = ld2(pv.q[1], o);
-            f2[F2] = ld2(pv.q[2], o);
+            const long long pb2 = plane(q + 2);
+            const int o2 = (wr && q + 2 >= kb && q + 2 < ke) ? col * 8 : ST_NOSTORE;
+            fx[F2] = ld2b(x + pb2, g.ps, o2);
+            f0[F2] = ld2b(pv.q[0] + pb2, g.ps, o2);
+            f1[F2] = ld2b(pv.q[1] + pb2, g.ps, o2);
+            f2[F2] = ld2b(pv.q[2] + pb2, g.ps, o2);
         }
+        __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
         // ---- a: p_it at q + 2 ----
         const double2 p2 = FIRST ? rr[S2] : fma2p(rr[S2], beta, po[S2]);
@@ -225,6 +266,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
                 st2b<false>(x + pb, g.ps, bo, xw);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     };
     int n = 0;
     for (; n + 3 < nsteps; n += 4) {
