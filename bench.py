@@ -692,14 +692,22 @@ def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
 
 
 def cg_variant_auto(n, world, case="cavity"):
-    """The bench's CG variant: the single-reduction z-march (k_ccf) where it is
-    measured faster than textbook CG, i.e. one GPU at 512^3 (1.17 vs 1.31 ms
-    per iteration); on the slab shapes of 2 / 4 / 8 ranks it is even or
-    slower (0.638 vs 0.645, 0.342 vs 0.324, 0.190 vs 0.162 ms: fewer z runs
-    leave the last round of workgroups part-empty), so slabs keep textbook CG
-    (profiles/r04_ccf_slab_shapes.jsonl). The Taylor-Green case keeps the
-    textbook CG its parity tests pin."""
-    return 1 if world == 1 and n >= 512 and case == "cavity" else 0
+    """The bench's CG variant: the single-reduction CG (projection_hip_cg1) for
+    the cavity wherever it is measured faster than textbook CG:
+    - one GPU at n >= 512: the fused march k_ccf (1.07-1.20 vs 1.31 ms per
+      iteration at 512^3, box-dependent; DESIGN.md section 3);
+    - Z-slabs (N > 1): the r05 fused slab form (edge planes, the r halo on the
+      side stream over the interior march, which also forms w and the dots,
+      then k_cc2 on the edge planes only) with ONE all-reduce per iteration,
+      the north star's design. Shared-GPU rehearsals at 512^3 (all ranks on
+      one device, profiles/r05_slab_rehearsal/): N = 2 124.7 vs 112.6 MLUPS,
+      N = 4 81.0 vs 70.4; on the N = 8 slab shape (66 planes) the march's
+      compute is 0.181 vs 0.163 ms per iteration (profiles/r05e_kc.jsonl)
+      against one all-reduce saved.
+    The Taylor-Green case keeps the textbook CG its parity tests pin."""
+    if case != "cavity":
+        return 0
+    return 1 if (world > 1 or n >= 512) else 0
 
 
 def prof_record(prof, kname):

@@ -42,6 +42,15 @@ namespace cfdhip {
 #endif
 constexpr int CCF_AHEAD = CFD_CCF_AHEAD;
 static_assert(CCF_AHEAD == 1 || CCF_AHEAD == 2, "k_ccf prefetch depth");
+// 1: stage c's LDS reads issued right after the barrier, ahead of stages a
+// and b (-DCFD_CCF_CFIRST=1); 0: after stage b. Measured equal at 512^3
+// (1.2616 vs 1.2610 ms per iteration, profiles/r05f_ccf_cfirst_ab.jsonl),
+// so the default keeps the 10 VGPRs the early reads hold (the fold form
+// would sit at 126 of 128)
+#ifndef CFD_CCF_CFIRST
+#define CFD_CCF_CFIRST 0
+#endif
+constexpr bool CCF_CFIRST = CFD_CCF_CFIRST != 0;
 constexpr int CCF_TC = 32;  // x pairs per tile row
 constexpr int CCF_TR = 32;  // tile rows
 constexpr int CCF_OX = 60;  // columns written per tile
@@ -60,11 +69,18 @@ struct CcfLds {
 // NOC (Z-slabs): no stage c; p_it is also stored on the slab's halo planes
 // (the next iteration forms p there from the exchanged r), and the r halo +
 // k_cc2<..., WST = false> complete the iteration with its one reduction.
+// That is the march of a slab's two edge planes (kmode 1), and of a whole
+// slab of < 3 planes. The interior planes of a slab (kmode 2) run the full
+// march (!NOC): stage c covers planes k0 + 1 .. k1 - 2, whose r_{it+1}
+// neighbours the march forms itself (the edge planes' r_{it+1} from the same
+// operands as the edge launch), and its partial dot products join the edge
+// planes' k_cc2 launch (g.part_ofs / part_total, dist = 1).
 template <bool FIRST, bool FOLD, bool NOC = false>
 static __global__ __launch_bounds__(1024, 4) void k_ccf(
     SGeo g, Lap Lp, const double* __restrict__ R0, double* __restrict__ R1,
     const double* __restrict__ Po, double* __restrict__ Pn, PPrev pv, double* __restrict__ x,
-    CgState* st, double* partials, unsigned* counter, int it, int xmap) {
+    CgState* st, double* partials, unsigned* counter, int it, int xmap, int dist, double* dsum,
+    Mbox* mb) {
     __shared__ CcfLds L;
     if (st->done) return;
     const double a = st->alpha[it % CG_XFOLD];
@@ -129,15 +145,28 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         const int row = q / CCF_LR, cc = q % CCF_LP;
         if (row == 0 || row == CCF_TR + 1 || cc == 0 || cc == CCF_LP - 1) L.pl[e / CCF_LS][q] = 0.0;
     }
-    // -A v at the pair from its own pair (v), its z neighbours and the plane's LDS
-    auto stencil = [&](int pl, double2 v, double2 zm, double2 zp, double2& out)
-                       __attribute__((always_inline)) {
-        const double lf = lrd(pl, LFo), rt = lrd(pl, RTo);
-        const double dx = lrd(pl, DNX), dy = lrd(pl, DNY);
-        const double ux = lrd(pl, UPX), uy = lrd(pl, UPY);
-        out.x = -lap7(Lp, v.x, lf, v.y, dx, ux, zm.x, zp.x);
-        out.y = -lap7(Lp, v.y, v.x, rt, dy, uy, zm.y, zp.y);
+    // the six in-plane neighbours of the pair in LDS plane pl
+    struct Nb {
+        double lf, rt, dx, dy, ux, uy;
     };
+    auto nbrs = [&](int pl) __attribute__((always_inline)) -> Nb {
+        Nb n;
+        n.lf = lrd(pl, LFo);
+        n.rt = lrd(pl, RTo);
+        n.dx = lrd(pl, DNX);
+        n.dy = lrd(pl, DNY);
+        n.ux = lrd(pl, UPX);
+        n.uy = lrd(pl, UPY);
+        return n;
+    };
+    // -A v at the pair from its own pair (v), its z neighbours and the in-plane ones
+    auto stencil_n = [&](const Nb& n, double2 v, double2 zm, double2 zp, double2& out)
+                         __attribute__((always_inline)) {
+        out.x = -lap7(Lp, v.x, n.lf, v.y, n.dx, n.ux, zm.x, zp.x);
+        out.y = -lap7(Lp, v.y, v.x, n.rt, n.dy, n.uy, zm.y, zp.y);
+    };
+    auto stencil = [&](int pl, double2 v, double2 zm, double2 zp, double2& out)
+                       __attribute__((always_inline)) { stencil_n(nbrs(pl), v, zm, zp, out); };
     const int q0 = kb - 4;  // steps q0 .. ke - 1 (see the header)
     const int nsteps = ke - kb + 4;
     // rings (slot of plane p at step q: (p - q0) & 3): r_it, p_{it-1} (loaded
@@ -214,6 +243,10 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         }
         __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
+        // stage c's in-plane operands (r_{it+1} of plane q, published last
+        // step) first: their LDS latency then overlaps stages a and b
+        Nb nc{};
+        if constexpr (!NOC && CCF_CFIRST) nc = nbrs(LRR);
         // ---- a: p_it at q + 2 ----
         const double2 p2 = FIRST ? rr[S2] : fma2p(rr[S2], beta, po[S2]);
         pn[S2] = p2;
@@ -226,11 +259,12 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         const double2 r1 = make_double2((kbin && in0) ? rv.x + ma * s.x : 0.0,
                                         (kbin && in1) ? rv.y + ma * s.y : 0.0);
         rn[S1] = r1;
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!CCF_CFIRST) __builtin_amdgcn_sched_barrier(0);
         // ---- c: w_{it+1} at q, the dot products ----
         if constexpr (!NOC) {
             double2 wv;
-            stencil(LRR, rn[S0], rn[SM], r1, wv);
+            if constexpr (CCF_CFIRST) stencil_n(nc, rn[S0], rn[SM], r1, wv);
+            else stencil(LRR, rn[S0], rn[SM], r1, wv);
             if (q >= kb && own) {
                 const double2 rc = rn[S0];
                 if (in0) {
@@ -296,8 +330,12 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         }
     double tg, td;
     double* shs = &L.pl[0][0];
-    if (grid_sum2_last<1024>(bg, bd, partials, counter, shs, &L.flag, tg, td) && threadIdx.x == 0)
-        fin_cc(st, tg, td, it, FOLD);
+    // g.part_total > 0: the interior planes of a Z-slab, whose reduction the
+    // edge planes' k_cc2 launch after the r halo completes (kernels.hpp)
+    if (grid_sum2_last<1024>(bg, bd, partials, counter, shs, &L.flag, tg, td,
+                             (unsigned)g.part_ofs, (unsigned)g.part_total) &&
+        threadIdx.x == 0)
+        cc_reduce_finish(st, tg, td, it, false, dist != 0, mb, dsum);
 }
 
 }  // namespace cfdhip

@@ -139,6 +139,9 @@ struct hip_proj_ctx {
     SGeo r2geo{};                        // two-iterations-per-sweep RB-SOR tiling (k_rb2)
     SGeo ccgeo{};                        // fused single-reduction CG tiling (k_ccf)
     SGeo cc_edge{}, cc_int{};            // slabs: k_ccf on the edge planes, then the rest
+    // slabs, fused form: cc_int with stage c and a shared reduction, and
+    // k_cc2's tiling of the two edge planes completing it (tiles_x 0: off)
+    SGeo cc_int_red{}, cc2_edge{};
     double* r2 = nullptr;                // k_ccf: r_{it+1} when r_it is in r (by parity)
     double* partials = nullptr;
     unsigned* counter = nullptr;

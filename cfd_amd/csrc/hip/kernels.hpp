@@ -1208,15 +1208,19 @@ static __global__ __launch_bounds__(256) void k_cc1(SGeo g, double* __restrict__
     }
 }
 
-// Two-value form of grid_sum_last_n (partials[b] and partials[gridDim.x + b]).
+// Two-value form of grid_sum_last_n (partials[pofs + b] and partials[nb +
+// pofs + b], nb = ptot, or gridDim.x when ptot is 0). With ptot > 0 several
+// launches on one stream share the reduction: this launch owns slots [pofs,
+// pofs + gridDim.x) of ptot, and the last of all ptot workgroups finishes.
 template <int NTH>
 __device__ __forceinline__ bool grid_sum2_last(double b0, double b1, double* partials,
                                                unsigned* counter, double* sh, int* flag,
-                                               double& t0, double& t1) {
-    const unsigned nb = gridDim.x;
+                                               double& t0, double& t1, unsigned pofs = 0,
+                                               unsigned ptot = 0) {
+    const unsigned nb = ptot ? ptot : gridDim.x;
     if (threadIdx.x == 0) {
-        store_sc1(&partials[blockIdx.x], b0);
-        store_sc1(&partials[nb + blockIdx.x], b1);
+        store_sc1(&partials[pofs + blockIdx.x], b0);
+        store_sc1(&partials[nb + pofs + blockIdx.x], b1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
@@ -1250,8 +1254,35 @@ __device__ __forceinline__ bool grid_sum2_last(double b0, double b1, double* par
     return true;
 }
 
+// The end of the single-reduction iteration's one reduction (the finishing
+// workgroup, thread 0): on Z-slabs the all-ranks sum through the device
+// mailbox, or left in dsum for an RCCL all-reduce + k_finish_cc; on one
+// device fin_cc0 / fin_cc directly.
+__device__ __forceinline__ void cc_reduce_finish(CgState* st, double tg, double td, int it,
+                                                 bool init, bool dist, Mbox* mb, double* dsum) {
+    if (dist && mb) {
+        double gg, gd;
+        if (mbox_allreduce2(mb, tg, td, &gg, &gd)) {
+            if (init) fin_cc0(st, gd);
+            else fin_cc(st, gg, gd, it, (it % CG_XFOLD) == CG_XFOLD - 1);
+        } else {
+            comm_fail(st);
+        }
+    } else if (dist) {
+        dsum[0] = tg;
+        dsum[1] = td;
+    } else if (init) {
+        fin_cc0(st, td);
+    } else {
+        fin_cc(st, tg, td, it, (it % CG_XFOLD) == CG_XFOLD - 1);
+    }
+}
+
 // w = A r on the row-pair tiling (k_cgA's stencil with p = r), written to w,
 // and the one reduction of iteration it: gamma = (r, r), delta = (w, r).
+// g.part_total > 0 (Z-slabs, the fused iteration): the launch covers the two
+// edge planes (kmode 1) and shares the reduction with the k_ccf launch of the
+// interior planes before it (its partials first).
 // INIT: the w = A r_0 before iteration 0 (fin_cc0; gamma_0 comes from setup).
 // WST = false (the fused iteration on Z-slabs, ccf.hpp): w stays in registers
 template <int TY, bool DIST, bool INIT, bool WST = true>
@@ -1325,25 +1356,10 @@ static __global__ __launch_bounds__(64 * TY) void k_cc2(SGeo g, Lap L,
         }
     double tg, td;
     double* shs = (double*)&rows[0][0][0];
-    if (grid_sum2_last<64 * TY>(bg, bd, partials, counter, shs, &flag, tg, td) &&
-        threadIdx.x == 0) {
-        if (DIST && mb) {
-            double gg, gd;
-            if (mbox_allreduce2(mb, tg, td, &gg, &gd)) {
-                if (INIT) fin_cc0(st, gd);
-                else fin_cc(st, gg, gd, it, (it % CG_XFOLD) == CG_XFOLD - 1);
-            } else {
-                comm_fail(st);
-            }
-        } else if (DIST) {
-            dsum[0] = tg;
-            dsum[1] = td;
-        } else if (INIT) {
-            fin_cc0(st, td);
-        } else {
-            fin_cc(st, tg, td, it, (it % CG_XFOLD) == CG_XFOLD - 1);
-        }
-    }
+    if (grid_sum2_last<64 * TY>(bg, bd, partials, counter, shs, &flag, tg, td,
+                                (unsigned)g.part_ofs, (unsigned)g.part_total) &&
+        threadIdx.x == 0)
+        cc_reduce_finish(st, tg, td, it, INIT, DIST, mb, dsum);
 }
 
 // ---------------------------------------------------------------------------

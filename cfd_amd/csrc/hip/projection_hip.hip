@@ -138,32 +138,37 @@ static void launch_cc1(hip_proj_ctx* c, double* pn, const double* po, const PPre
 }
 
 template <int TY, bool DIST, bool INIT, bool WST>
-static void launch_cc2_t(hip_proj_ctx* c, const Lap& L, int it, const double* r) {
-    hipExtLaunchKernelGGL((k_cc2<TY, DIST, INIT, WST>), dim3(sweep_grid(c)), dim3(64 * TY), 0,
-                          c->stream, c->ta, c->tb, 0, c->sgeo, L, r, c->cw, c->st, c->partials,
+static void launch_cc2_t(hip_proj_ctx* c, const SGeo& g, const Lap& L, int it, const double* r) {
+    const unsigned nb = (unsigned)(g.tiles_x * g.tiles_y * g.tiles_z);
+    hipExtLaunchKernelGGL((k_cc2<TY, DIST, INIT, WST>), dim3(nb), dim3(64 * TY), 0,
+                          c->stream, c->ta, c->tb, 0, g, L, r, c->cw, c->st, c->partials,
                           c->counter, it, c->dsum, mbox(c));
 }
 
 template <int TY, bool WST>
-static void launch_cc2_w(hip_proj_ctx* c, const Lap& L, int it, bool init, const double* r) {
-    if (dist(c)) init ? launch_cc2_t<TY, true, true, WST>(c, L, it, r)
-                      : launch_cc2_t<TY, true, false, WST>(c, L, it, r);
-    else init ? launch_cc2_t<TY, false, true, WST>(c, L, it, r)
-              : launch_cc2_t<TY, false, false, WST>(c, L, it, r);
+static void launch_cc2_w(hip_proj_ctx* c, const SGeo& g, const Lap& L, int it, bool init,
+                         const double* r) {
+    if (dist(c)) init ? launch_cc2_t<TY, true, true, WST>(c, g, L, it, r)
+                      : launch_cc2_t<TY, true, false, WST>(c, g, L, it, r);
+    else init ? launch_cc2_t<TY, false, true, WST>(c, g, L, it, r)
+              : launch_cc2_t<TY, false, false, WST>(c, g, L, it, r);
 }
 
 template <int TY>
-static void launch_cc2_ty(hip_proj_ctx* c, const Lap& L, int it, bool init, const double* r,
-                          bool wst) {
-    wst ? launch_cc2_w<TY, true>(c, L, it, init, r) : launch_cc2_w<TY, false>(c, L, it, init, r);
+static void launch_cc2_ty(hip_proj_ctx* c, const SGeo& g, const Lap& L, int it, bool init,
+                          const double* r, bool wst) {
+    wst ? launch_cc2_w<TY, true>(c, g, L, it, init, r)
+        : launch_cc2_w<TY, false>(c, g, L, it, init, r);
 }
 
-// w = A r (stored for k_cc1 when wst) and the iteration's one reduction
+// w = A r (stored for k_cc1 when wst) and the iteration's one reduction, over
+// the planes of g (c->sgeo: all of them; c->cc2_edge: a slab's edge planes)
 static void launch_cc2(hip_proj_ctx* c, const Lap& L, int it, bool init, const double* r,
-                       bool wst) {
-    if (c->sweep_ty == 16) return launch_cc2_ty<16>(c, L, it, init, r, wst);
-    if (c->sweep_ty == 4) return launch_cc2_ty<4>(c, L, it, init, r, wst);
-    return launch_cc2_ty<8>(c, L, it, init, r, wst);
+                       bool wst, const SGeo* gp = nullptr) {
+    const SGeo& g = gp ? *gp : c->sgeo;
+    if (c->sweep_ty == 16) return launch_cc2_ty<16>(c, g, L, it, init, r, wst);
+    if (c->sweep_ty == 4) return launch_cc2_ty<4>(c, g, L, it, init, r, wst);
+    return launch_cc2_ty<8>(c, g, L, it, init, r, wst);
 }
 
 // k_ccf (ccf.hpp): cg_variant 1's whole iteration in one z-march; r_it is in
@@ -179,7 +184,8 @@ static void launch_ccf_t(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* p
                          const double* po, const PPrev& pv, double* x, int it, int xmap) {
     hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD, NOC>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
                           dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, ccf_r0(c, it),
-                          ccf_r1(c, it), po, pn, pv, x, c->st, c->partials, c->counter, it, xmap);
+                          ccf_r1(c, it), po, pn, pv, x, c->st, c->partials, c->counter, it, xmap,
+                          dist(c) ? 1 : 0, c->dsum, mbox(c));
 }
 
 template <bool NOC>
@@ -191,11 +197,14 @@ static void launch_ccf_n(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* p
     else launch_ccf_t<false, false, NOC>(c, g, L, pn, po, pv, x, it, xmap);
 }
 
-// g: c->ccgeo (the whole march), or on Z-slabs c->cc_edge / c->cc_int
+// g: c->ccgeo (the whole march), or on Z-slabs c->cc_edge / c->cc_int. noc:
+// the march stops after r_{it+1} (Z-slab edge planes, or a whole slab of < 3
+// planes), else it also forms w and the dot products (one device; a slab's
+// interior planes in the fused form)
 static void launch_ccf(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
-                       const double* po, const PPrev& pv, double* x, int it) {
+                       const double* po, const PPrev& pv, double* x, int it, bool noc) {
     static const int xmap = getenv("CFD_HIP_CCF_XMAP") ? atoi(getenv("CFD_HIP_CCF_XMAP")) : 0;
-    if (dist(c)) launch_ccf_n<true>(c, g, L, pn, po, pv, x, it, xmap);
+    if (noc) launch_ccf_n<true>(c, g, L, pn, po, pv, x, it, xmap);
     else launch_ccf_n<false>(c, g, L, pn, po, pv, x, it, xmap);
 }
 
@@ -326,17 +335,23 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         PPrev pv;
         for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];
         if (ccf && !D) {
-            timed(c, HIP_KT_CC_FUSED, [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it); },
-                  it);
+            timed(c, HIP_KT_CC_FUSED,
+                  [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it, false); }, it);
             return CFD_SUCCESS;
         }
         if (ccf) {
             // Z-slabs: r_{it+1} on the two edge planes first; its halo then
             // travels on the side stream (halo communicator) while the march
-            // covers the interior planes; the SpMV + reduction wait for it
+            // covers the interior planes; the SpMV + reduction wait for it.
+            // Fused form (default): the interior march also forms w and the
+            // dot products of planes k0 + 1 .. k1 - 2, so k_cc2 covers only the
+            // two edge planes (whose w needs the neighbours' r) and completes
+            // the shared reduction; CFD_HIP_CCF_SLAB_FUSED=0: k_cc2 over every
+            // plane (r04)
             double* r1 = ccf_r1(c, it);
             if (c->cc_edge.tiles_x > 0) {
-                launch_ccf(c, c->cc_edge, L, pnew, pold, pv, x, it);
+                const bool fused = c->cc2_edge.tiles_x > 0;
+                launch_ccf(c, c->cc_edge, L, pnew, pold, pv, x, it, true);
                 HIP_TRY(hipEventRecord(c->ev_b, c->stream));
                 HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
                 double* rr[1] = {r1};
@@ -345,14 +360,18 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                 }, it));
                 HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
                 timed(c, HIP_KT_CC_FUSED,
-                      [&] { launch_ccf(c, c->cc_int, L, pnew, pold, pv, x, it); }, it);
+                      [&] { launch_ccf(c, fused ? c->cc_int_red : c->cc_int, L, pnew, pold, pv,
+                                       x, it, !fused); }, it);
                 HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
+                timed(c, HIP_KT_CC_SPMV, [&] {
+                    launch_cc2(c, L, it, false, r1, false, fused ? &c->cc2_edge : nullptr);
+                }, it);
             } else {
                 timed(c, HIP_KT_CC_FUSED,
-                      [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it); }, it);
+                      [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it, true); }, it);
                 ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {r1}); }, it));
+                timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false, r1, false); }, it);
             }
-            timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false, r1, false); }, it);
             return reduce_cc(it, false);
         }
         timed(c, HIP_KT_CC_UPDATE, [&] { launch_cc1(c, pnew, pold, pv, x, it); }, it);
@@ -1339,6 +1358,26 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
                 m.kt1 = cg.k1 - 1;
                 m.kc = std::max(1, std::min(cg.kc, m.kt1 - m.kt0));
                 m.tiles_z = (m.kt1 - m.kt0 + m.kc - 1) / m.kc;
+                // fused form: the interior march with stage c (cc_int_red)
+                // and k_cc2 on the two edge planes (cc2_edge, the row-pair
+                // tiling of k_cc2 in kmode 1) share one reduction, the
+                // interior workgroups' partials first
+                const char* ef = getenv("CFD_HIP_CCF_SLAB_FUSED");
+                if (!(ef && atoi(ef) == 0)) {
+                    SGeo& ir = c->cc_int_red;
+                    SGeo& ee = c->cc2_edge;
+                    ir = m;
+                    ee = sg;
+                    ee.kmode = 1;
+                    ee.kc = 1;
+                    ee.tiles_z = 2;
+                    const int ni = ir.tiles_x * ir.tiles_y * ir.tiles_z;
+                    const int ne = ee.tiles_x * ee.tiles_y * ee.tiles_z;
+                    ir.part_ofs = 0;
+                    ee.part_ofs = ni;
+                    ir.part_total = ee.part_total = ni + ne;
+                    n_partials = std::max(n_partials, ni + ne);
+                }
             }
         }
         // the last x tile of a TC-64 launch is partial unless 124 divides the
