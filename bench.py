@@ -246,7 +246,8 @@ def main():
 
     kt = ctx.timing()
     sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s, total ms)
-    sweep_set = sweep_kernels(args.sweep_rows, world > 1, args.sweep_variant, args.cg_variant)
+    sweep_set = sweep_kernels(args.sweep_rows, world > 1, args.sweep_variant, args.cg_variant,
+                              ctx.nz_local - 2)
     for key, kname, bpc in sweep_set:
         ms, cnt = kt[key]
         avg = ms / cnt if cnt else None
@@ -645,7 +646,7 @@ TIMER_KERNEL = {"predictor": "k_pred2<false, 0>" if _PC_OLD else "k_pred3<false,
                 "cg_setup": "k_cg_setup<true, false, true, false>"}
 
 
-def sweep_kernels(rows, dist_, variant, cg_variant):
+def sweep_kernels(rows, dist_, variant, cg_variant, planes=None):
     """(timer, kernel symbol as rocprofv3 prints it, algorithmic B/cell) of the
     CG sweeps a run launches; the symbols key the committed PMC profile."""
     d = "true" if dist_ else "false"
@@ -656,10 +657,14 @@ def sweep_kernels(rows, dist_, variant, cg_variant):
         # the fold launches, so the byte count is their mean
         return (("cc_fused", "k_ccf<false, false, false>", BYTES_CC_FUSED),)
     if cg_variant == 1:
-        # Z-slabs: the march up to r_{it+1}, the r halo, then w = A r in
-        # registers with the one reduction (k_cc2 without the w store)
-        return (("cc_fused", "k_ccf<false, false, true>", BYTES_CC_FUSED),
-                ("cc_spmv", f"k_cc2<{rows}, {d}, false, false>", BYTES_CC_SPMV_NOW))
+        # Z-slabs, fused form (r05): the edge planes' march (k_ccf<.., true>,
+        # untimed, 2 planes), the r halo, the interior march with w and the
+        # dots (the timer), then w = A r in registers on the two edge planes
+        # completing the one reduction (k_cc2 without the w store): its bytes
+        # per slab cell are 8 B x 2 / planes
+        return (("cc_fused", "k_ccf<false, false, false>", BYTES_CC_FUSED),
+                ("cc_spmv", f"k_cc2<{rows}, {d}, false, false>",
+                 BYTES_CC_SPMV_NOW * 2.0 / planes if planes else BYTES_CC_SPMV_NOW))
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
             ("cg_sweep_b", f"k_cgB<{rows}, {d}, {variant}, {rev}>", BYTES_SWEEP_B),
             ("cg_sweep_bx", f"k_cgA<{rows}, false, {d}, {variant & ~4}, true>", BYTES_SWEEP_AX))

@@ -600,13 +600,12 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     cf.kb = rc.rdx2 + rc.rdy2 + rc.inv_dz2;
     cf.escale = 1.0;
     cf.mlim = 0x1p800;
-    cf.slow = -899;
-    cf.pad = 0;
+    cf.slow = 0x1p-900;
     if (const char* e = getenv("CFD_HIP_RB2_TEST")) {  // tests: force the host paths
         const int v = atoi(e);
         if (v == 1) cf.escale = 1e300;  // every approximate decision ambiguous
         if (v == 2) cf.mlim = 0.0;      // every sweep uncertified
-        if (v == 3) cf.slow = 100000;   // every SOR update in the reference's arithmetic
+        if (v == 3) cf.slow = 1e300;    // every SOR update in the reference's arithmetic
     }
     // the fast division's range argument (rb2.hpp rb2_sorc) needs 1 <= 1/d^2 <= 2^60
     if (!(rc.rdx2 >= 1.0 && rc.rdy2 >= 1.0 && rc.rdx2 <= 0x1p60 && rc.rdy2 <= 0x1p60))

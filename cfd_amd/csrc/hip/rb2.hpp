@@ -77,11 +77,11 @@ struct Rb2Coef {
     double kb;   // 1/dx2 + 1/dy2 + inv_dz2 (error bound)
     // test knobs (CFD_HIP_RB2_TEST): escale multiplies the residual bound
     // (1e300: every decision ambiguous); mlim is the largest certified
-    // |value| (2^800; 0: every sweep uncertified); slow is the least binary
-    // exponent of a divided neighbour sum the fast division takes (-899;
-    // 100000: every SOR update recomputed in the reference's arithmetic)
+    // |value| (2^800; 0: every sweep uncertified); slow: a wave recomputes an
+    // SOR update in the reference's arithmetic when the smaller |neighbour
+    // sum| of one of its lanes is below it (2^-900; 1e300: every update)
     double escale, mlim;
-    int slow, pad;
+    double slow;
 };
 
 // LDS of one k_rb2 workgroup (148 KB): X by plane parity, and the one-colour
@@ -161,24 +161,32 @@ __device__ __forceinline__ double rb2_max_abs2(double a, double b) {
     return r;
 }
 
+__device__ __forceinline__ double rb2_min_abs2(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // One SOR update, APX: the fast divisions, with their range test folded into
 // ONE wave-uniform branch per update. The fast quotient is correctly rounded
 // for |a r| in [2^-900, 2^900] or a = 0 (divz); the sweep certifies |v| <=
 // 2^800 for every value (so |sx|, |sy| <= 2^801, and 1 <= 1/d^2 <= 2^60 is
-// checked on the host), and here a wave in which some neighbour sum is
-// nonzero with |sum| < 2^-900 (binary exponent < -899: the zero-valued front
-// of a solve from a zero guess leaves such values) recomputes the update with
-// divc. Either way the value is the reference's.
+// checked on the host), and here a wave in which some neighbour sum has
+// |sum| < 2^-900 (the zero-valued front of a solve from a zero guess leaves
+// such values) recomputes the update with divc. The test is min(|sx|, |sy|)
+// < 2^-900: two instructions (r05; the binary-exponent form, two frexp + min
+// + compare, also let exact zeros take the fast path, which is exact for
+// them, and costs two more per update). Either way the value is the
+// reference's.
 template <bool APX>
-__device__ __forceinline__ double rb2_sorc(const RelaxCoef& rc, int slow, double vc, double sx,
-                                           double sy, double sz, double vb,
+__device__ __forceinline__ double rb2_sorc(const RelaxCoef& rc, double slow, double vc,
+                                           double sx, double sy, double sz, double vb,
                                            double* tout = nullptr) {
     if constexpr (!APX) {
         return rb2_sor<false>(rc, vc, sx, sy, sz, vb, tout);
     } else {
         double v = rb2_sor<true>(rc, vc, sx, sy, sz, vb, tout);
-        const int ex = min(rb2_exp(sx), rb2_exp(sy));
-        if (__builtin_amdgcn_ballot_w64(ex < slow) != 0)
+        if (__builtin_amdgcn_ballot_w64(rb2_min_abs2(sx, sy) < slow) != 0)
             v = rb2_sor<false>(rc, vc, sx, sy, sz, vb, tout);
         return v;
     }

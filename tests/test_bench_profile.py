@@ -28,11 +28,13 @@ def test_profile_is_current_and_complete():
 
 
 def test_cg_variant_auto_and_fused_record():
-    # single-reduction only where it is measured faster: one GPU at 512^3
+    # single-reduction where it is measured faster: one GPU at 512^3, and
+    # Z-slabs (the fused slab form, one all-reduce per iteration)
     assert bench.cg_variant_auto(512, 1) == 1
     assert bench.cg_variant_auto(256, 1) == 0
-    assert all(bench.cg_variant_auto(512, w) == 0 for w in (2, 4, 8))
+    assert all(bench.cg_variant_auto(512, w) == 1 for w in (2, 4, 8))
     assert bench.cg_variant_auto(512, 1, "tg") == 0
+    assert bench.cg_variant_auto(512, 8, "tg") == 0
     # the fused timer's bytes: launch-weighted over k_ccf<*, *, false> only
     prof = {"kernels": {
         "k_ccf<true, false, false>": {"calls": 1, "hbm_bytes_per_launch": 10.0},
@@ -52,6 +54,8 @@ def test_sweep_symbols_track_the_variant():
     # Z-slabs the march without its last stage + k_cc2 without the w store
     cc = dict((t, k) for t, k, _ in bench.sweep_kernels(16, False, 15, 1))
     assert cc == {"cc_fused": "k_ccf<false, false, false>"}
-    ccd = dict((t, k) for t, k, _ in bench.sweep_kernels(16, True, 15, 1))
-    assert ccd == {"cc_fused": "k_ccf<false, false, true>",
+    ccd = dict((t, k) for t, k, _ in bench.sweep_kernels(16, True, 15, 1, 64))
+    assert ccd == {"cc_fused": "k_ccf<false, false, false>",
                    "cc_spmv": "k_cc2<16, true, false, false>"}
+    # the edge planes' k_cc2: 8 B per edge-plane cell, per slab cell 8 x 2 / planes
+    assert dict((t, b) for t, _, b in bench.sweep_kernels(16, True, 15, 1, 64))["cc_spmv"] == 0.25
