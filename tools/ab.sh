@@ -13,6 +13,26 @@
 # Output: gpurun_out/<TAG>/{pytest_<v>.log, ab.jsonl, pmc.jsonl}.
 # usage: TAG=rev SW=CFD_HIP_CGB_REV VALUES="0 1" TESTS="tests/test_gpu_parity.py" \
 #        CMD="python3 tools/relax_bench.py" tools/ab.sh
+#
+# Recorded experiments in this form (the measuring programs are the
+# tools/*_bench.py; a build under test is selected with CFD_AMD_HIP_LIB =
+# cfd_amd/lib_ab/<name>/libcfd_hip.so, built by `make -C cfd_amd/csrc
+# OUT=.../lib_ab/<name> OBJ=.../build_ab/<name> HIPCC="hipcc -D..."`):
+#   k_ccf memory-op order / prefetch depth / stage-c reads (r05):
+#     SW=CFD_AMD_HIP_LIB VALUES="<base> <variant> -" TESTS=tests/test_gpu_cg_single_reduction.py
+#     SHAPES=512 VARIANTS=1 ITERS=200 CMD="python3 tools/cg_variant_bench.py"
+#   k_ccf z-run length (r04, r05): SW=CFD_HIP_CCF_KC VALUES="- 16 24" (+ CFD_HIP_CCF_KC_FIXED=1
+#     for slab shapes, SHAPES=slabs), same CMD
+#   k_ccf tile order vs fetched bytes (r04): SW=CFD_HIP_CCF_XMAP VALUES="0 1", then
+#     PASSES="fetch write" CMD="python3 tools/cg_variant_bench.py" tools/pmc_passes.sh
+#   k_rb2 range test (r05), tile map / run length (r04): SW=CFD_AMD_HIP_LIB or
+#     CFD_HIP_RB2_XMAP / CFD_HIP_RB2_KC, TESTS="tests/test_gpu_rb2.py
+#     tests/test_gpu_convection_tol.py", NX=1024 NY=1024 NZ=512 ITERS=40 METHODS=rbsor
+#     CMD="python3 tools/relax_bench.py"; k_rb1 vs k_rb2: SW=CFD_HIP_RB2 VALUES="0 1 2"
+#   corrector / sweep-store variants (r04): SW=CFD_HIP_PC3 VALUES="1 5 6"
+#     CMD="python3 tools/step_kernels_bench.py"
+#   slab CG forms at N ranks on one shared GPU: tools/slab_rehearsal.sh
+#   configs[4] trace + FETCH/WRITE + step: tools/conv_profile.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-ab}

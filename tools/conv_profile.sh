@@ -5,7 +5,7 @@
 # reads it for roofline.traffic.
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
 mkdir -p gpurun_out
-TAG=${TAG:-r04_conv}
+TAG=${TAG:-conv}
 CELLS=$((1022*1022*510)) TAG=$TAG ARGS="--case convection --steps 1 --warmup 0 --relax-max-iter 200 --allow-max-iter --no-cpu-baseline" bash tools/gpu_profile.sh || exit 1
 cp gpurun_out/prof_${TAG}/traffic.json profiles/${TAG}_traffic.json || exit 1
 timeout -k 10 600 python bench.py --case convection --steps 1 --warmup 0 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err

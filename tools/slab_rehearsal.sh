@@ -5,7 +5,7 @@
 # bench.py at N ranks for textbook CG (cg_variant 0) and the single-reduction
 # CG (1; fused slab form, and CFD_HIP_CCF_SLAB_FUSED=0 the r04 form). The
 # ranks share one GPU, so the numbers compare the forms' total device work
-# and synchronisation, not an 8-GPU node's xGMI. usage: NS="2 4 8" TESTS=1
+# and synchronisation, not an 8-GPU node's xGMI. usage: TAG=r05h NS="2 4 8" TESTS=1 CFD_BENCH_SHARED_GPU=1 tools/slab_rehearsal.sh
 set -o pipefail
 O=gpurun_out/${TAG:-r05g}; mkdir -p $O
 if [ -n "$TESTS" ]; then
