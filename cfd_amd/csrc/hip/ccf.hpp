@@ -51,6 +51,15 @@ static_assert(CCF_AHEAD == 1 || CCF_AHEAD == 2, "k_ccf prefetch depth");
 #define CFD_CCF_CFIRST 0
 #endif
 constexpr bool CCF_CFIRST = CFD_CCF_CFIRST != 0;
+// Diagnostic builds only (wrong results; never the product): -DCFD_CCF_DIAG=1
+// every load reads plane 0 (cache-resident) and no store reaches memory;
+// 2: no in-plane stencil (no LDS reads, no stencil arithmetic). Both ignore
+// the done flag so that every launch runs its whole march. They split the
+// iteration's time into its memory and its synchronised-compute parts.
+#ifndef CFD_CCF_DIAG
+#define CFD_CCF_DIAG 0
+#endif
+constexpr int CCF_DIAG = CFD_CCF_DIAG;
 constexpr int CCF_TC = 32;  // x pairs per tile row
 constexpr int CCF_TR = 32;  // tile rows
 constexpr int CCF_OX = 60;  // columns written per tile
@@ -82,7 +91,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     CgState* st, double* partials, unsigned* counter, int it, int xmap, int dist, double* dsum,
     Mbox* mb) {
     __shared__ CcfLds L;
-    if (st->done) return;
+    if (CCF_DIAG == 0 && st->done) return;
     const double a = st->alpha[it % CG_XFOLD];
     const double ma = -a;
     const double beta = FIRST ? 0.0 : st->beta;
@@ -123,7 +132,9 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     // cells' values, which only feed cells outside the interior (masked)
     const int ic = i0 < 0 ? 0 : (i0 < g.nx ? i0 : g.nx - 2 - ((g.nx - 2) & 1));
     const int col = max(min(j, g.ny - 1), 0) * (int)g.px + ic;
-    auto plane = [&](int k) -> long long { return (long long)min(max(k, 0), g.nz - 1) * g.ps; };
+    auto plane = [&](int k) -> long long {
+        return CCF_DIAG == 1 ? 0LL : (long long)min(max(k, 0), g.nz - 1) * g.ps;
+    };
     // LDS: one base at the lane's cell minus one row and one column of the
     // padded plane, so every operand is a non-negative immediate offset
     double* const Lb = &L.pl[0][r * CCF_LR + c];
@@ -166,7 +177,14 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         out.y = -lap7(Lp, v.y, v.x, n.rt, n.dy, n.uy, zm.y, zp.y);
     };
     auto stencil = [&](int pl, double2 v, double2 zm, double2 zp, double2& out)
-                       __attribute__((always_inline)) { stencil_n(nbrs(pl), v, zm, zp, out); };
+                       __attribute__((always_inline)) {
+        if constexpr (CCF_DIAG == 2) {
+            out.x = v.x + zm.x + zp.x;
+            out.y = v.y + zm.y + zp.y;
+        } else {
+            stencil_n(nbrs(pl), v, zm, zp, out);
+        }
+    };
     const int q0 = kb - 4;  // steps q0 .. ke - 1 (see the header)
     const int nsteps = ke - kb + 4;
     // rings (slot of plane p at step q: (p - q0) & 3): r_it, p_{it-1} (loaded
@@ -282,10 +300,10 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
         if constexpr (!NOC) lput(LRW, r1);
         {
             const bool qown = qb >= kb && qb < ke;
-            const int bo = (qown && wr) ? col * 8 : ST_NOSTORE;
+            const int bo = (qown && wr && CCF_DIAG != 1) ? col * 8 : ST_NOSTORE;
             // NOC: p also on the halo plane below / above the slab's owned planes
             const bool qhalo = NOC && ((qb == kb - 1 && kb == g.k0) || (qb == ke && ke == g.k1));
-            const int bp = ((qown || qhalo) && wr) ? col * 8 : ST_NOSTORE;
+            const int bp = ((qown || qhalo) && wr && CCF_DIAG != 1) ? col * 8 : ST_NOSTORE;
             const long long pb = plane(qb);
             const double2 p1 = pn[S1];
             st2b<false>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
