@@ -60,6 +60,22 @@ constexpr bool CCF_CFIRST = CFD_CCF_CFIRST != 0;
 #define CFD_CCF_DIAG 0
 #endif
 constexpr int CCF_DIAG = CFD_CCF_DIAG;
+// non-temporal stores of p_it, r_{it+1} and x (-DCFD_CCF_NTST=1, A/B builds)
+// (r05: 1.132 -> 1.085 ms per iteration at 512^3, profiles/r05l_ccf_ntst_ab.jsonl:
+// p, r and x are next read a whole iteration later, far beyond the caches,
+// and written through they no longer displace the halo lines the
+// neighbouring tiles re-read). -DCFD_CCF_NTST=0: plain stores
+#ifndef CFD_CCF_NTST
+#define CFD_CCF_NTST 1
+#endif
+constexpr bool CCF_NTST = CFD_CCF_NTST != 0;
+// non-temporal loads of the fold operands (x, p_{it-3..it-1}: read once, by
+// the storing lanes only) with -DCFD_CCF_NTFOLD=1: measured slower (1.188 vs
+// 1.156 ms per iteration, profiles/r05m_ccf_ntfold_ab.jsonl), so plain loads
+#ifndef CFD_CCF_NTFOLD
+#define CFD_CCF_NTFOLD 0
+#endif
+constexpr bool CCF_NTFOLD = CFD_CCF_NTFOLD != 0;
 constexpr int CCF_TC = 32;  // x pairs per tile row
 constexpr int CCF_TR = 32;  // tile rows
 constexpr int CCF_OX = 60;  // columns written per tile
@@ -254,10 +270,10 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
             // vs 1.159 ms per iteration at 512^3, profiles/r04_ccf_fold_owned_loads_ab.jsonl
             const long long pb2 = plane(q + 2);
             const int o2 = (wr && q + 2 >= kb && q + 2 < ke) ? col * 8 : ST_NOSTORE;
-            fx[F2] = ld2b(x + pb2, g.ps, o2);
-            f0[F2] = ld2b(pv.q[0] + pb2, g.ps, o2);
-            f1[F2] = ld2b(pv.q[1] + pb2, g.ps, o2);
-            f2[F2] = ld2b(pv.q[2] + pb2, g.ps, o2);
+            fx[F2] = ld2b<CCF_NTFOLD>(x + pb2, g.ps, o2);
+            f0[F2] = ld2b<CCF_NTFOLD>(pv.q[0] + pb2, g.ps, o2);
+            f1[F2] = ld2b<CCF_NTFOLD>(pv.q[1] + pb2, g.ps, o2);
+            f2[F2] = ld2b<CCF_NTFOLD>(pv.q[2] + pb2, g.ps, o2);
         }
         __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
@@ -306,8 +322,8 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
             const int bp = ((qown || qhalo) && wr && CCF_DIAG != 1) ? col * 8 : ST_NOSTORE;
             const long long pb = plane(qb);
             const double2 p1 = pn[S1];
-            st2b<false>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
-            st2b<false>(R1 + pb, g.ps, bo, r1);
+            st2b<CCF_NTST>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
+            st2b<CCF_NTST>(R1 + pb, g.ps, bo, r1);
             if (FOLD) {
                 const double2 xo = fx[F1], qa = f0[F1], qq = f1[F1], qc = f2[F1];
                 double2 xw;
@@ -315,7 +331,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
                            : xo.x;
                 xw.y = in1 ? (((xo.y + aq[0] * qa.y) + aq[1] * qq.y) + aq[2] * qc.y) + a * p1.y
                            : xo.y;
-                st2b<false>(x + pb, g.ps, bo, xw);
+                st2b<CCF_NTST>(x + pb, g.ps, bo, xw);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
