@@ -106,6 +106,8 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     const double* __restrict__ Po, double* __restrict__ Pn, PPrev pv, double* __restrict__ x,
     CgState* st, double* partials, unsigned* counter, int it, int xmap, int dist, double* dsum,
     Mbox* mb) {
+    // (a fold step reads p_{it-1} from the po ring, which FIRST never loads)
+    static_assert(!(FIRST && FOLD), "k_ccf: no fold in the first iteration");
     __shared__ CcfLds L;
     if (CCF_DIAG == 0 && st->done) return;
     const double a = st->alpha[it % CG_XFOLD];
@@ -206,11 +208,11 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     // rings (slot of plane p at step q: (p - q0) & 3): r_it, p_{it-1} (loaded
     // one step ahead), p_it, r_{it+1}; fold operands (x, p_{it-3..it-1}) by parity
     double2 rr[4], po[4], pn[4], rn[4];
-    double2 fx[2], f0[2], f1[2], f2[2];
+    double2 fx[2], f0[2], f1[2];
     const double2 zero = make_double2(0.0, 0.0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) pn[s] = rn[s] = po[s] = rr[s] = zero;
-    fx[0] = fx[1] = f0[0] = f0[1] = f1[0] = f1[1] = f2[0] = f2[1] = zero;
+    fx[0] = fx[1] = f0[0] = f0[1] = f1[0] = f1[1] = zero;
     // (r_it of plane q0 + 1 = kb - 3 only feeds r_{it+1} there, never used)
     // (the fold operands of plane q0 + 1 = kb - 3 are never stored: no load)
     // Each prologue load is followed by dropped stores in the place of a
@@ -270,10 +272,12 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
             // vs 1.159 ms per iteration at 512^3, profiles/r04_ccf_fold_owned_loads_ab.jsonl
             const long long pb2 = plane(q + 2);
             const int o2 = (wr && q + 2 >= kb && q + 2 < ke) ? col * 8 : ST_NOSTORE;
+            // (p_{it-1}, the fold's third pending direction, is the march's
+            // own p_{it-1} ring (po), still holding plane q + 1 when step q
+            // folds it: no load of its own, r05)
             fx[F2] = ld2b<CCF_NTFOLD>(x + pb2, g.ps, o2);
             f0[F2] = ld2b<CCF_NTFOLD>(pv.q[0] + pb2, g.ps, o2);
             f1[F2] = ld2b<CCF_NTFOLD>(pv.q[1] + pb2, g.ps, o2);
-            f2[F2] = ld2b<CCF_NTFOLD>(pv.q[2] + pb2, g.ps, o2);
         }
         __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
@@ -325,7 +329,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
             st2b<CCF_NTST>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
             st2b<CCF_NTST>(R1 + pb, g.ps, bo, r1);
             if (FOLD) {
-                const double2 xo = fx[F1], qa = f0[F1], qq = f1[F1], qc = f2[F1];
+                const double2 xo = fx[F1], qa = f0[F1], qq = f1[F1], qc = po[S1];
                 double2 xw;
                 xw.x = in0 ? (((xo.x + aq[0] * qa.x) + aq[1] * qq.x) + aq[2] * qc.x) + a * p1.x
                            : xo.x;
