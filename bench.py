@@ -50,8 +50,9 @@ BYTES_SWEEP_AX = 64.0   # every 4th iteration, sweep A + read x, p_{it-4..it-2};
 BYTES_CC_UPDATE = 66.0  # cg_variant 1, k_cc1: read r, w, p_old, s; write p, s, r (56) + x fold / 4
 BYTES_CC_SPMV = 16.0    # cg_variant 1, k_cc2: read r (stencil); write w
 BYTES_CC_SPMV_NOW = 8.0 # cg_variant 1 on Z-slabs, k_cc2 without the w store: read r (stencil)
-BYTES_CC_FUSED = 42.0   # cg_variant 1, k_ccf: read r, p_old; write p, r (32)
-                        # + the x fold's 40 B every 4th iteration (mean per iteration)
+BYTES_CC_FUSED = 40.0   # cg_variant 1, k_ccf: read r, p_old; write p, r (32)
+                        # + the x fold's 32 B every 4th iteration (read x, p_{it-3},
+                        # p_{it-2}; write x; p_{it-1} is the march's own p_old)
 BYTES_CG_SMALL_ITER = 64.0    # small grids, k_cg_small per iteration (x updated every iteration)
 BYTES_CG_ITER_SURVEY = 80.0   # SURVEY.md §8d textbook CG iteration (x, r, p, Ap)
 BYTES_STEP_FIXED_SURVEY = 176.0  # SURVEY.md §8d per-step non-CG bytes
@@ -676,7 +677,7 @@ BYTES_CG_TEXTBOOK = 58.0  # textbook CG per iteration: sweeps A + B (48) + the x
 def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
     """ms per iteration of `iters` CG iterations (no early exit, x0 = 0) on the
     context's last step's RHS and on cos_rhs, with the algorithmic rate in
-    both byte models (42 B/cell: the single-reduction march; 58: textbook)."""
+    both byte models (40 B/cell: the single-reduction march; 58: textbook)."""
     rho_over_dt = 1.0 / params.dt  # rho = 1 (the cavity)
     out = {"bytes_per_cell_moved": BYTES_CC_FUSED if cg_variant == 1 else BYTES_CG_TEXTBOOK}
     for name, rhs in (("step_rhs", None), ("cos_rhs", cos_rhs)):
@@ -689,7 +690,7 @@ def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
             continue
         per = ms / iters
         out[name] = {"ms_per_iter": round(per, 4),
-                     "GBps_42": round(BYTES_CC_FUSED * n_int / (per * 1e-3) / 1e9, 1),
+                     "GBps_40": round(BYTES_CC_FUSED * n_int / (per * 1e-3) / 1e9, 1),
                      "GBps_58": round(BYTES_CG_TEXTBOOK * n_int / (per * 1e-3) / 1e9, 1),
                      "frac_of_8TBps_own_bytes": round(out["bytes_per_cell_moved"] * n_int
                                                       / (per * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
