@@ -21,12 +21,16 @@ def main():
         return
     tot = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
+    dur = defaultdict(dict)  # kernel -> dispatch -> ns
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"].split("(")[0]
                 tot[k][row["Counter_Name"]] += float(row["Counter_Value"])
-                disp[k].add((f.name, row.get("Dispatch_Id", row.get("Correlation_Id", ""))))
+                d = (f.name, row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+                disp[k].add(d)
+                if row.get("Start_Timestamp") and row.get("End_Timestamp"):
+                    dur[k][d] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
     if note:
         print(json.dumps({"note": note}))
     for k, c in sorted(tot.items(), key=lambda kv: -sum(kv[1].values())):
@@ -34,6 +38,15 @@ def main():
         out = {name: round(v / n, 1) for name, v in sorted(c.items())}
         out["kernel"] = k
         out["launches"] = n
+        if dur[k]:
+            # mean profiled duration; with GRBM_GUI_ACTIVE (summed over the 8
+            # XCDs) the effective clock of the pass (MI355X_MICROARCH.md,
+            # DVFS give-back: reads high below ~0.3 ms per dispatch)
+            ns = sum(dur[k].values()) / len(dur[k])
+            out["dur_us"] = round(ns / 1e3, 2)
+            ga = c.get("GRBM_GUI_ACTIVE")
+            if ga and ns > 0:
+                out["eff_clock_GHz"] = round(ga / n / 8 / ns, 3)
         wc = c.get("SQ_WAVE_CYCLES")
         if wc:
             for name in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
