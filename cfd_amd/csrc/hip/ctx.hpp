@@ -157,6 +157,20 @@ struct hip_proj_ctx {
     size_t bytes = 0;
     std::vector<void*> allocs;  // hipMalloc bases of the field arrays
     size_t stagger_bytes = 0;
+    // Environment switches of the solve paths, read ONCE when the context
+    // is created (init_ctx), never per step or per solve: rank threads of an
+    // in-process group would otherwise call getenv while another thread of
+    // the process (a test fixture, the runtime) may change the environment,
+    // and getenv is not safe against a concurrent setenv / putenv. Tests set
+    // the variables before they create contexts.
+    struct {
+        bool ccf_off = false;     // CFD_HIP_CCF=0: k_cc1 + k_cc2 instead of k_ccf
+        int cg_small = -1;        // CFD_HIP_CG_SMALL (-1 unset, 0 never, 1 up to 1M cells)
+        int rb2_test = 0;         // CFD_HIP_RB2_TEST: force k_rb2's host paths
+        int rb2_xmap = 0;         // CFD_HIP_RB2_XMAP (experiments)
+        bool rb2_log = false;     // CFD_HIP_RB2_LOG (diagnostics)
+        int rb2 = 1;              // CFD_HIP_RB2: 1 certified fast, 2 exact, 0 k_rb1
+    } env;
     // timing
     int timing = 0;
     std::vector<hipEvent_t> ev_pool;

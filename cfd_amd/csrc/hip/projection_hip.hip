@@ -317,9 +317,8 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     // k_cc2 (w = A r and both dots, ONE reduction / all-reduce)
     const bool cc = (c->cfg.cg_variant == 1);
     // 3-D: the fused iteration (k_ccf; on Z-slabs + the r halo + k_cc2);
-    // CFD_HIP_CCF = 0 keeps k_cc1 + k_cc2 (read per solve: tests switch it)
-    const char* eccf = getenv("CFD_HIP_CCF");
-    const bool ccf = cc && c->ccgeo.tiles_x > 0 && !(eccf && atoi(eccf) == 0);
+    // CFD_HIP_CCF = 0 keeps k_cc1 + k_cc2 (c->env: read at context creation)
+    const bool ccf = cc && c->ccgeo.tiles_x > 0 && !c->env.ccf_off;
     auto reduce_cc = [&](int it, bool init) -> cfd_status_t {
         if (!D || mbox(c)) return CFD_SUCCESS;
         return timed_span(c, c->stream, HIP_KT_ALLREDUCE, [&] {
@@ -399,8 +398,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
     const long long ncell = (long long)(c->nx - 2) * (long long)(c->ny - 2) *
                             (long long)(c->geo.k1 - c->geo.k0);
     {
-        const char* e = getenv("CFD_HIP_CG_SMALL");
-        const int mode = e ? atoi(e) : -1;
+        const int mode = c->env.cg_small;
         const long long cap = (mode == 1) ? (long long)CGS_MAX_WG * CGS_THREADS * 16
                                           : (mode == 0 ? 0 : CG_SMALL_CELLS);
         if (!D && !cc && max_iter > 0 && ncell > 0 && ncell <= cap) {
@@ -601,8 +599,8 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     cf.escale = 1.0;
     cf.mlim = 0x1p800;
     cf.slow = 0x1p-900;
-    if (const char* e = getenv("CFD_HIP_RB2_TEST")) {  // tests: force the host paths
-        const int v = atoi(e);
+    if (c->env.rb2_test) {  // tests: force the host paths
+        const int v = c->env.rb2_test;
         if (v == 1) cf.escale = 1e300;  // every approximate decision ambiguous
         if (v == 2) cf.mlim = 0.0;      // every sweep uncertified
         if (v == 3) cf.slow = 1e300;    // every SOR update in the reference's arithmetic
@@ -612,7 +610,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         apx = false;
     constexpr int FLR = SW_NT_STORE | SW_PREFETCH | SW_EDGE1;
     const SGeo& g2 = c->r2geo;
-    const int xmap = getenv("CFD_HIP_RB2_XMAP") ? atoi(getenv("CFD_HIP_RB2_XMAP")) : 0;
+    const int xmap = c->env.rb2_xmap;
     const unsigned nb2 = (unsigned)(g2.tiles_x * g2.tiles_y * g2.tiles_z);
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
                           rel_tol, abs_tol, max_iter, 1);
@@ -741,7 +739,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         flush_timing(c);
         double res = r.res;
         if (!r.res_exact) ST_TRY(residual_linf(c, xt, resc, &res));
-        if (getenv("CFD_HIP_RB2_LOG")) {  // diagnostics: the loop's launches and stops
+        if (c->env.rb2_log) {  // diagnostics: the loop's launches and stops
             int n1 = 0, n2 = 0;
             for (const Launch& q : log) (q.kind == 1 ? n1 : n2)++;
             fprintf(stderr, "rb2: iterations %d status %d, k_rb1 %d k_rb2 %d launches, "
@@ -821,10 +819,9 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     // two iterations per sweep on one device (rb2.hpp): CFD_HIP_RB2 = 1 (the
     // default: certified fast arithmetic), 2 (the reference's arithmetic
     // throughout), 0 (one iteration per sweep, k_rb1)
-    const int rb2_env = getenv("CFD_HIP_RB2") ? atoi(getenv("CFD_HIP_RB2")) : 1;
+    const int rb2_env = c->env.rb2;
     if (neu_fold && !D && check_interval == 1 && rb2_env != 0 && c->r2geo.tiles_x > 0)
         return relax_solve_rb2(c, rc, rel_tol, abs_tol, max_iter, rb2_env != 2);
-    const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
     ST_TRY(halo(c, {c->pn}));
     hipExtLaunchKernelGGL(k_rx_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0, c->rxst,
                           rel_tol, abs_tol, max_iter, check_interval);
@@ -1189,6 +1186,18 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     HIP_TRY(hipGetDeviceProperties(&prop, c->device));
     c->grid_cap = std::max(64, prop.multiProcessorCount * 8);
     if (const char* e = getenv("CFD_HIP_FIELD_STAGGER")) c->stagger_bytes = (size_t)atol(e) / 256 * 256;
+    {
+        auto ienv = [](const char* name, int dflt) {
+            const char* e = getenv(name);
+            return e ? atoi(e) : dflt;
+        };
+        c->env.ccf_off = ienv("CFD_HIP_CCF", 1) == 0;
+        c->env.cg_small = ienv("CFD_HIP_CG_SMALL", -1);
+        c->env.rb2_test = ienv("CFD_HIP_RB2_TEST", 0);
+        c->env.rb2_xmap = ienv("CFD_HIP_RB2_XMAP", 0);
+        c->env.rb2_log = getenv("CFD_HIP_RB2_LOG") != nullptr;
+        c->env.rb2 = ienv("CFD_HIP_RB2", 1);
+    }
     c->nx = nx;
     c->ny = ny;
     c->nz = nz;
@@ -1909,7 +1918,7 @@ static cfd_status_t step_device_impl(hip_proj_ctx_t* c, const grid* g,
     cfd_status_t s = ctx_validate_params(c, g, prm);
     if (s != CFD_SUCCESS) return s;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t nx = c->nx, ny = c->ny, nz = c->nzg;
+    const size_t nz = c->nzg;
     const double dx = g->dx[0], dy = g->dy[0];
     const double dz = (nz > 1 && g->dz) ? g->dz[0] : 0.0;
     const double dt = prm->dt;

@@ -97,6 +97,15 @@ __global__ __launch_bounds__(256) void k_shell_io(FieldSet fs, int nf, ShellMap 
 // Host side of the same layout over caller arrays (nx*ny*nz, packed), split
 // over threads by rows: the partial rows touch two cache lines each, 4 KB or
 // more apart, which one core walks at a fraction of the copy rate.
+// CFD_HIP_SHELL_THREADS (experiments), read once per process
+static int shell_threads_env() {
+    static const int n = [] {
+        const char* e = getenv("CFD_HIP_SHELL_THREADS");
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
+    return n;
+}
+
 void host_rows(const ShellMap& m, int nf, double* const* host, double* buf, bool gather) {
     const long long nrows = m.ny * m.nz * nf;
     const long long total = m.total();
@@ -126,7 +135,7 @@ void host_rows(const ShellMap& m, int nf, double* const* host, double* buf, bool
     const long long cells = total * nf;
     unsigned hc = std::thread::hardware_concurrency();
     int nt = (int)std::min<unsigned>(hc ? hc : 1, 16);
-    if (const char* e = getenv("CFD_HIP_SHELL_THREADS")) nt = std::max(1, atoi(e));
+    if (shell_threads_env() > 0) nt = shell_threads_env();
     if (cells < (1LL << 18)) nt = 1;
     if (nt == 1) {
         work(0, nrows);
@@ -217,7 +226,7 @@ void ctx_host_hash(const hip_proj_ctx* c, const double* const* host, int nf, boo
     const long long planes = k1 - k0;
     unsigned hc = std::thread::hardware_concurrency();
     int nt = (int)std::min<unsigned>(hc ? hc : 1, 16);
-    if (const char* e = getenv("CFD_HIP_SHELL_THREADS")) nt = std::max(1, atoi(e));
+    if (shell_threads_env() > 0) nt = shell_threads_env();
     if (layer1) nt = std::min(nt, 4);
     nt = (int)std::max(1LL, std::min<long long>(nt, planes));
     auto mix = [](const double* p, long long idx) {
