@@ -733,17 +733,22 @@ def prof_record(prof, kname):
 
 def pmc_profile(cells):
     """The newest committed PMC profile (profiles/*_traffic*.json, written by
-    tools/prof_summary.py) taken on the current HIP sources and this grid, or
-    None: a profile of other kernel code is never used."""
-    from cfd_amd._native import kernel_source_sha
+    tools/prof_summary.py) taken on this grid with the kernels this run loads
+    -- the same HIP sources, or the same device code in the library
+    (cfd_amd._sha.device_code_sha: host-only edits keep it) -- or None: a
+    profile of other kernel code is never used."""
+    from cfd_amd._native import HIP_LIB, kernel_source_sha
+    from cfd_amd._sha import device_code_sha
 
     sha = kernel_source_sha()
+    dev = device_code_sha(HIP_LIB)
     for path in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
         try:
             d = json.loads(path.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("source_sha") == sha and d.get("cells_per_launch") == float(cells):
+        same = d.get("source_sha") == sha or (dev is not None and d.get("device_sha") == dev)
+        if same and d.get("cells_per_launch") == float(cells):
             d["file"] = path.name
             return d
     return None

@@ -105,10 +105,12 @@ def main():
                     rec["hbm_bytes_per_cell"] = rec["hbm_bytes_per_launch"] / cells
             out[k] = rec
         sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-        from cfd_amd._native import kernel_source_sha
+        from cfd_amd._native import HIP_LIB, kernel_source_sha
+        from cfd_amd._sha import device_code_sha
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as fh:
             json.dump({"source": str(d), "correction": "2*FETCH_SIZE + WRITE_SIZE",
                        "source_sha": kernel_source_sha(),
+                       "device_sha": device_code_sha(HIP_LIB),
                        "cells_per_launch": cells, "kernels": out}, fh, indent=1)
 
 
