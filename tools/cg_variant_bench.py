@@ -26,6 +26,8 @@ def main():
     shapes = [(512, 512, 512), (512, 512, 66)]
     if os.environ.get("SHAPES") == "512":  # profiling runs: the cube only
         shapes = shapes[:1]
+    elif os.environ.get("SHAPES") == "thin":  # rank 0's slab of 512^3 on 2, 4, 8 ranks
+        shapes = [(512, 512, 257), (512, 512, 130), (512, 512, 66)]
     elif os.environ.get("SHAPES") == "slabs":  # rank 0's slab of 512^3 on 1, 2, 4, 8 ranks
         shapes = [(512, 512, 512), (512, 512, 257), (512, 512, 130), (512, 512, 66)]
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
