@@ -69,6 +69,11 @@ constexpr int CCF_DIAG = CFD_CCF_DIAG;
 #define CFD_CCF_NTST 1
 #endif
 constexpr bool CCF_NTST = CFD_CCF_NTST != 0;
+// the stores' full cache-policy bits (A/B builds: -DCFD_CCF_STAUX=N)
+#ifndef CFD_CCF_STAUX
+#define CFD_CCF_STAUX (CFD_CCF_NTST ? 2 : 0)
+#endif
+constexpr int CCF_STAUX = CFD_CCF_STAUX;
 // non-temporal loads of the fold operands (x, p_{it-3..it-1}: read once, by
 // the storing lanes only) with -DCFD_CCF_NTFOLD=1: measured slower (1.188 vs
 // 1.156 ms per iteration, profiles/r05m_ccf_ntfold_ab.jsonl), so plain loads
@@ -326,8 +331,8 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
             const int bp = ((qown || qhalo) && wr && CCF_DIAG != 1) ? col * 8 : ST_NOSTORE;
             const long long pb = plane(qb);
             const double2 p1 = pn[S1];
-            st2b<CCF_NTST>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
-            st2b<CCF_NTST>(R1 + pb, g.ps, bo, r1);
+            st2ba<CCF_STAUX>(Pn + pb, g.ps, bp, make_double2(in0 ? p1.x : 0.0, in1 ? p1.y : 0.0));
+            st2ba<CCF_STAUX>(R1 + pb, g.ps, bo, r1);
             if (FOLD) {
                 const double2 xo = fx[F1], qa = f0[F1], qq = f1[F1], qc = po[S1];
                 double2 xw;
@@ -335,7 +340,7 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
                            : xo.x;
                 xw.y = in1 ? (((xo.y + aq[0] * qa.y) + aq[1] * qq.y) + aq[2] * qc.y) + a * p1.y
                            : xo.y;
-                st2b<CCF_NTST>(x + pb, g.ps, bo, xw);
+                st2ba<CCF_STAUX>(x + pb, g.ps, bo, xw);
             }
         }
         __builtin_amdgcn_sched_barrier(0);

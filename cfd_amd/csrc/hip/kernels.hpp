@@ -450,16 +450,22 @@ __device__ __forceinline__ void st2v(double* p, long long i, double2 v) {
 // counting stays exact (a store under a branch counts as possibly absent, so
 // the wait for a later plane's loads would also wait for that store).
 constexpr int ST_NOSTORE = 0x7ffffff0;
-template <bool NT>
-__device__ __forceinline__ void st2b(double* plane_base, long long plane_elems, int boff,
-                                     double2 v) {
+// AUX: the store's cache-policy bits (2: nt, 16: sc1 write-through)
+template <int AUX>
+__device__ __forceinline__ void st2ba(double* plane_base, long long plane_elems, int boff,
+                                      double2 v) {
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(plane_base, 0, (int)(plane_elems * 8), 0x00020000);
     const unsigned long long bx = (unsigned long long)__double_as_longlong(v.x);
     const unsigned long long by = (unsigned long long)__double_as_longlong(v.y);
     const u4 d = {(unsigned)bx, (unsigned)(bx >> 32), (unsigned)by, (unsigned)(by >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(d, rs, boff, 0, NT ? 2 : 0);  // aux 2: nt
+    __builtin_amdgcn_raw_buffer_store_b128(d, rs, boff, 0, AUX);
+}
+template <bool NT>
+__device__ __forceinline__ void st2b(double* plane_base, long long plane_elems, int boff,
+                                     double2 v) {
+    st2ba<NT ? 2 : 0>(plane_base, plane_elems, boff, v);  // aux 2: nt
 }
 
 // The load counterpart of st2b: a 16-B load from one plane through a buffer
