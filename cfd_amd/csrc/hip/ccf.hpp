@@ -74,6 +74,11 @@ constexpr bool CCF_NTST = CFD_CCF_NTST != 0;
 #define CFD_CCF_STAUX (CFD_CCF_NTST ? 2 : 0)
 #endif
 constexpr int CCF_STAUX = CFD_CCF_STAUX;
+// the march's r_it / p_{it-1} loads' cache-policy bits (A/B: -DCFD_CCF_LDAUX=N)
+#ifndef CFD_CCF_LDAUX
+#define CFD_CCF_LDAUX 0
+#endif
+constexpr int CCF_LDAUX = CFD_CCF_LDAUX;
 // non-temporal loads of the fold operands (x, p_{it-3..it-1}: read once, by
 // the storing lanes only) with -DCFD_CCF_NTFOLD=1: measured slower (1.188 vs
 // 1.156 ms per iteration, profiles/r05m_ccf_ntfold_ab.jsonl), so plain loads
@@ -225,8 +230,8 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     // same ops as every later step's (the loop header joins both paths).
     auto pro = [&](int k) __attribute__((always_inline)) {
         const int s = (k - q0) & 3;
-        rr[s] = ld2b(R0 + plane(k), g.ps, col * 8);
-        if (!FIRST) po[s] = ld2b(Po + plane(k), g.ps, col * 8);
+        rr[s] = ld2ba<CCF_LDAUX>(R0 + plane(k), g.ps, col * 8);
+        if (!FIRST) po[s] = ld2ba<CCF_LDAUX>(Po + plane(k), g.ps, col * 8);
         st2b<false>(Pn, g.ps, ST_NOSTORE, zero);
         st2b<false>(R1, g.ps, ST_NOSTORE, zero);
         if (FOLD) st2b<false>(x, g.ps, ST_NOSTORE, zero);
@@ -268,8 +273,8 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
             const int ql = q + CCF_AHEAD + 2;
             const long long pbl = plane(ql);
             const int ol = (ql <= ke + 1) ? col * 8 : ST_NOSTORE;
-            rr[SL] = ld2b(R0 + pbl, g.ps, ol);
-            if (!FIRST) po[SL] = ld2b(Po + pbl, g.ps, ol);
+            rr[SL] = ld2ba<CCF_LDAUX>(R0 + pbl, g.ps, ol);
+            if (!FIRST) po[SL] = ld2ba<CCF_LDAUX>(Po + pbl, g.ps, ol);
         }
         if (FOLD) {
             // only the lanes and planes that store x read its operands (the

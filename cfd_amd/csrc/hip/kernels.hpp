@@ -472,15 +472,21 @@ __device__ __forceinline__ void st2b(double* plane_base, long long plane_elems, 
 // resource; an offset past the plane (ST_NOSTORE) returns zeros without a
 // memory access, so a lane or step that needs no data issues the same load
 // instead of branching around it (no branch: exact vmcnt counting).
-template <bool NT = false>
-__device__ __forceinline__ double2 ld2b(const double* plane_base, long long plane_elems, int boff) {
+// AUX: the load's cache-policy bits (2: nt, 16: sc1, which bypasses the L1)
+template <int AUX>
+__device__ __forceinline__ double2 ld2ba(const double* plane_base, long long plane_elems,
+                                         int boff) {
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<double*>(plane_base), 0, (int)(plane_elems * 8), 0x00020000);
-    const u4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, NT ? 2 : 0);  // aux 2: nt
+    const u4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, AUX);
     const unsigned long long bx = (unsigned long long)d.x | ((unsigned long long)d.y << 32);
     const unsigned long long by = (unsigned long long)d.z | ((unsigned long long)d.w << 32);
     return make_double2(__longlong_as_double((long long)bx), __longlong_as_double((long long)by));
+}
+template <bool NT = false>
+__device__ __forceinline__ double2 ld2b(const double* plane_base, long long plane_elems, int boff) {
+    return ld2ba<NT ? 2 : 0>(plane_base, plane_elems, boff);  // aux 2: nt
 }
 
 template <int FL>
