@@ -691,6 +691,9 @@ def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
         per = ms / iters
         out[name] = {"ms_per_iter": round(per, 4),
                      "GBps_40": round(BYTES_CC_FUSED * n_int / (per * 1e-3) / 1e9, 1),
+                     # r04's count for the march (before the fold read p_{it-1}
+                     # from its own registers), the key the r04 review named
+                     "GBps_42": round(42.0 * n_int / (per * 1e-3) / 1e9, 1),
                      "GBps_58": round(BYTES_CG_TEXTBOOK * n_int / (per * 1e-3) / 1e9, 1),
                      "frac_of_8TBps_own_bytes": round(out["bytes_per_cell_moved"] * n_int
                                                       / (per * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
