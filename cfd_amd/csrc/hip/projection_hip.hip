@@ -1573,6 +1573,22 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
         free_ctx(c);
         return nullptr;
     }
+    if (comm && c->cfg.poisson_method != HIP_POISSON_CG) {
+        // Z-slab ranks of a relaxation solver: what the first solve would set
+        // up lazily on a rank thread (the aux fields, the loop state, the
+        // library's code object, which a kernel attribute query loads) is set
+        // up here, at creation
+        hipFuncAttributes fa;
+        bool ok = hipFuncGetAttributes(&fa, (const void*)k_rx_init) == hipSuccess &&
+                  ensure_aux(c, true, true) == CFD_SUCCESS;
+        if (ok && !c->rxst) ok = hipMalloc((void**)&c->rxst, sizeof(RxState)) == hipSuccess;
+        if (ok && !c->rxst2) ok = hipMalloc((void**)&c->rxst2, sizeof(RxState)) == hipSuccess;
+        if (!ok) {
+            set_err(CFD_ERROR_NOMEM, "projection_hip: slab relaxation setup failed");
+            free_ctx(c);
+            return nullptr;
+        }
+    }
     return c;
 }
 
