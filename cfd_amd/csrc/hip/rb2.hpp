@@ -64,6 +64,10 @@
 
 namespace cfdhip {
 
+#ifndef CFD_RB2_DIAG
+#define CFD_RB2_DIAG 0
+#endif
+constexpr bool RB2_DIAG = CFD_RB2_DIAG != 0;
 constexpr int RB2_TC = 32;   // x pairs per tile row
 constexpr int RB2_TR = 32;   // tile rows (two per wave)
 constexpr int RB2_OX = 56;   // columns written per tile
@@ -284,10 +288,15 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     const int colx = max(min(j, g.ny - 1), 0) * (int)g.px + ic;
     const int col = max(min(j, g.ny - 1), 0) * (int)g.px + max(i0, 0);
     const int px = (int)g.px;
+    // RB2_DIAG (diagnostic builds only, wrong results): every load reads
+    // plane 0 (cache-resident) and the steady steps' stores are dropped,
+    // which splits a sweep's time into its memory and its on-chip part
     auto ldx = [&](int k) -> double2 {
+        if constexpr (RB2_DIAG) return ld2(X, colx);
         return ld2(X + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
     };
     auto ldr = [&](int k) -> double2 {
+        if constexpr (RB2_DIAG) return ld2(rhs, colx);
         return ld2(rhs + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
     };
     auto comp = [](const double2& v, int e) __attribute__((always_inline)) {
@@ -546,7 +555,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             // steady step of an interior tile: one store, never branched
             // around (st2b), so the loads' vmcnt waits exclude it
             st2b<(FL & SW_NT_STORE) != 0>(Y + (long long)qd * g.ps, g.ps,
-                                          own ? col * 8 : ST_NOSTORE, out);
+                                          (own && !RB2_DIAG) ? col * 8 : ST_NOSTORE, out);
         } else if (okd) {
             // the Neumann shell folded into the stores (as k_rb1)
             if (nrole & 1) out.x = out.y;
