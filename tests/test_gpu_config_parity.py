@@ -52,7 +52,8 @@ def omp_oracle():
     oracle.set_threads(1)
 
 
-def _steps(g, f, p, n_steps, bc, method=A.HIP_POISSON_CG, okind=A.ORACLE_POISSON_CG, **cfg):
+def _steps(g, f, p, n_steps, bc, method=A.HIP_POISSON_CG, okind=A.ORACLE_POISSON_CG,
+           it_tol=None, **cfg):
     fo, fh = _clone(g, f), _clone(g, f)
     ctx = api.HipProjection(g.nx, g.ny, g.nz, poisson_method=method, **cfg)
     its = []
@@ -67,7 +68,7 @@ def _steps(g, f, p, n_steps, bc, method=A.HIP_POISSON_CG, okind=A.ORACLE_POISSON
             assert sh == A.CFD_SUCCESS, (sh, api._native.last_error())
             ih = ctx.poisson_stats().iterations
             its.append((ih, io))
-            tol = 1 if method == A.HIP_POISSON_CG else 0
+            tol = it_tol if it_tol is not None else (1 if method == A.HIP_POISSON_CG else 0)
             assert abs(ih - io) <= tol, (ih, io)
             assert sth.max_velocity == pytest.approx(sto.max_velocity, rel=1e-9, abs=1e-300)
             assert sth.max_pressure == pytest.approx(sto.max_pressure, rel=1e-9, abs=1e-300)
@@ -84,6 +85,35 @@ def test_config1_tg256_vs_oracle(hip_lib, omp_oracle):
     for k in ("u", "v", "w", "p"):
         assert _rel(getattr(fh, k), getattr(fo, k)) <= CG_FIELD_RTOL, k
     assert all(i > 100 for i, _ in its), its  # a real solve at this size
+
+
+def test_config1_tg256_single_reduction_vs_oracle(hip_lib, omp_oracle):
+    """configs[1] at its size with the single-reduction CG (cg_variant 1, the
+    registered projection_hip_cg1; on one device the k_ccf march): periodic
+    BCs before each step, 2 steps against the oracle's textbook CG. Measured
+    (r05, profiles/r05ah_pytest_config_parity.log): identical iteration
+    counts (572, 506), fields within 2.4e-14; gated at the textbook CG's
+    bars (iterations within 1, fields 1e-10)."""
+    g, f, p = cases.tg3(256)
+    fo, fh = _clone(g, f), _clone(g, f)
+    ctx = api.HipProjection(g.nx, g.ny, g.nz, cg_variant=1)
+    try:
+        for _ in range(2):
+            cases.tg3_bc(fo)
+            cases.tg3_bc(fh)
+            so, sto, io = oracle.projection_step(fo, g, p, A.ORACLE_POISSON_CG)
+            sth = A.SolverStats()
+            sh = ctx.step(fh, g, p, sth)
+            assert so == sh == A.CFD_SUCCESS, (so, sh, api._native.last_error())
+            ih = ctx.poisson_stats().iterations
+            print("tg256 cg1 iterations", ih, io)
+            assert abs(ih - io) <= 1 and ih > 100, (ih, io)
+    finally:
+        ctx.close()
+    for k in ("u", "v", "w", "p"):
+        rel = _rel(getattr(fh, k), getattr(fo, k))
+        print("tg256 cg1", k, rel)
+        assert rel <= CG_FIELD_RTOL, (k, rel)
 
 
 def test_config2_cavity_re1000_vs_oracle(hip_lib, omp_oracle):
@@ -108,6 +138,18 @@ def test_density_branches_cg(hip_lib, rho):
         g1, f1, p1 = cases.cavity(33, 29, 21, Re=100.0, dt=5e-4)
         _, f1h, _ = _steps(g1, f1, p1, 3, lambda ff: api.cavity_bc(ff, 1.0))
         assert _rel(f1h.p, fh.p) > 1e-3
+
+
+@pytest.mark.parametrize("rho", [1.3, 1e-12])
+def test_density_branches_single_reduction_cg(hip_lib, rho):
+    """The density branches through the single-reduction CG (cg_variant 1,
+    k_ccf): the same RHS and corrector (the setup and corrector kernels are
+    shared), the single-reduction gates (iterations within 2, fields 1e-8)."""
+    g, f, p = cases.cavity(33, 29, 21, Re=100.0, dt=5e-4)
+    f.rho[...] = rho
+    fo, fh, _ = _steps(g, f, p, 3, lambda ff: api.cavity_bc(ff, 1.0), it_tol=2, cg_variant=1)
+    for k in ("u", "v", "w", "p"):
+        assert _rel(getattr(fh, k), getattr(fo, k)) <= 1e-8, k
 
 
 @pytest.mark.parametrize("rho", [1.3, 1e-12])
