@@ -125,6 +125,15 @@ def test_config2_cavity_re1000_vs_oracle(hip_lib, omp_oracle):
         assert _rel(getattr(fh, k), getattr(fo, k)) <= CG_FIELD_RTOL, k
 
 
+def test_config2_cavity_re1000_single_reduction_vs_oracle(hip_lib, omp_oracle):
+    """configs[2]'s physics at 128^3 through the single-reduction CG (the
+    bench's solver), 2 steps, at the textbook CG's bars."""
+    g, f, p = cases.cavity(128, 128, 128, Re=1000.0, dt=1e-4)
+    fo, fh, _ = _steps(g, f, p, 2, lambda ff: api.cavity_bc(ff, 1.0), cg_variant=1)
+    for k in ("u", "v", "w", "p"):
+        assert _rel(getattr(fh, k), getattr(fo, k)) <= CG_FIELD_RTOL, k
+
+
 @pytest.mark.parametrize("rho", [1.3, 1e-12])
 def test_density_branches_cg(hip_lib, rho):
     """rhs = (rho/dt) div u*, u = u* - (dt/rho) grad p with rho = rho[0], and
