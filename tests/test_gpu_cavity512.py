@@ -211,20 +211,23 @@ def test_cavity512_cg1_plugin_vs_oracle(hip_lib):
 
 
 @pytest.mark.timeout(900)
-def test_cavity512_slabs8_vs_oracle(hip_lib, monkeypatch):
+@pytest.mark.parametrize("cgv,nsteps", [(0, 6), (1, 3)], ids=["textbook", "single_reduction"])
+def test_cavity512_slabs8_vs_oracle(hip_lib, monkeypatch, cgv, nsteps):
     """configs[3]'s decomposition at its real slab depth (VERDICT r03 item
     3): the same trajectory on 8 in-process Z-slab ranks (64 planes each,
-    6 x 64 + 2 x 63 interior planes), steps 1-6 against the fixture with the
+    6 x 64 + 2 x 63 interior planes) against the fixture with the
     single-device bars; every rank's CG statistics must agree (one all-ranks
-    reduction per dot product)."""
+    reduction per dot product). Textbook CG steps 1-6; the single-reduction
+    CG (cg_variant 1, what bench.py runs at N > 1: the fused slab form, one
+    all-reduce per iteration) steps 1-3."""
     monkeypatch.setenv("CFD_HIP_GROUP_TIMEOUT_S", "120")
     rec = _fixture()
-    steps = rec["steps"][:6]
+    steps = rec["steps"][:nsteps]
     g = api.Grid(N, N, N, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
     params = api.validation_params(rec["dt"], 1.0 / rec["re"])
     nr = 8
     grp = api.LocalGroup(nr)
-    ctxs = [api.HipProjection(N, N, N, comm=grp.comm(r, 0)) for r in range(nr)]
+    ctxs = [api.HipProjection(N, N, N, comm=grp.comm(r, 0), cg_variant=cgv) for r in range(nr)]
     assert [c.nz_local - 2 for c in ctxs] == [64] * 6 + [63] * 2
     try:
         api.run_ranks(lambda r: _init(ctxs[r]), nr)  # BCs are per-rank collective calls
@@ -260,8 +263,8 @@ def test_cavity512_slabs8_vs_oracle(hip_lib, monkeypatch):
         for c in ctxs:
             c.close()
         grp.close()
-    print("cavity512 on 8 slabs, CG iterations (device, oracle):", its)
-    print("cavity512 on 8 slabs, largest deviations from the oracle:", worst)
+    print(f"cavity512 on 8 slabs (cg_variant {cgv}), CG iterations (device, oracle):", its)
+    print(f"cavity512 on 8 slabs (cg_variant {cgv}), largest deviations from the oracle:", worst)
 
 
 def test_cavity512_rccl2_vs_oracle(hip_lib, tmp_path):
