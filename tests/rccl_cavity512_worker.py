@@ -33,7 +33,8 @@ def main():
     comm = api.SlabComm.rccl(uid[0], RANK, WORLD, 0)
     g = api.Grid(N, N, N, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0)
     params = api.validation_params(1e-4, 1e-3)
-    ctx = api.HipProjection(N, N, N, comm=comm)
+    ctx = api.HipProjection(N, N, N, comm=comm,
+                            cg_variant=int(os.environ.get("CFD_CAV512_CG_VARIANT", "0")))
     for fid in FIDS.values():
         ctx.fill(fid, 0.0)
     ctx.set_density(1.0)

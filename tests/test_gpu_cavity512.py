@@ -267,12 +267,14 @@ def test_cavity512_slabs8_vs_oracle(hip_lib, monkeypatch, cgv, nsteps):
     print(f"cavity512 on 8 slabs (cg_variant {cgv}), largest deviations from the oracle:", worst)
 
 
-def test_cavity512_rccl2_vs_oracle(hip_lib, tmp_path):
+@pytest.mark.parametrize("cgv", [0, 1], ids=["textbook", "single_reduction"])
+def test_cavity512_rccl2_vs_oracle(hip_lib, tmp_path, cgv):
     """Steps 1-2 of the trajectory on 2 RCCL ranks (one process per rank,
     sharing the device through RCCL's socket transport) with the device
     mailbox all-reduce of the CG dot products on (tests/rccl_cavity512_worker.py):
     per-rank CG statistics, interior norms from the ranks' partial sums and
-    the sampled planes each rank owns, against the fixture."""
+    the sampled planes each rank owns, against the fixture; textbook CG and
+    the single-reduction CG (bench.py's solver at N > 1)."""
     import os
     import subprocess
     import sys
@@ -284,6 +286,7 @@ def test_cavity512_rccl2_vs_oracle(hip_lib, tmp_path):
     env["CFD_HIP_DEVICE_ALLREDUCE"] = "1"
     out = tmp_path / "rccl512.json"
     env["CFD_CAV512_OUT"] = str(out)
+    env["CFD_CAV512_CG_VARIANT"] = str(cgv)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
            str(root / "tests" / "rccl_cavity512_worker.py")]
