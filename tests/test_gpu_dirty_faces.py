@@ -154,17 +154,19 @@ def test_failed_step_returns_whole_field(hip_lib):
     cr.close()
 
 
-def test_plugin_env_switch(hip_lib, monkeypatch):
-    """CFD_HIP_DIRTY_FACES=N through the registry's projection_hip `step`:
-    a full download every N steps, equal to the default plugin's field."""
+@pytest.mark.parametrize("name", ["projection_hip", "projection_hip_cg1"])
+def test_plugin_env_switch(hip_lib, monkeypatch, name):
+    """CFD_HIP_DIRTY_FACES=N through the registry's `step` (the textbook-CG
+    plugin and the single-reduction one): a full download every N steps,
+    equal to the same plugin's field without the resident mode."""
     monkeypatch.setenv("CFD_HIP_DIRTY_FACES", "2")
     g, f, p = cases.cavity(21, 19, 17)
     fr = _clone(g, f)
     reg = api.Registry()
-    s_res = reg.create("projection_hip")
+    s_res = reg.create(name)
     assert s_res.init(g, p) == A.CFD_SUCCESS
     monkeypatch.delenv("CFD_HIP_DIRTY_FACES")
-    s_full = reg.create("projection_hip")
+    s_full = reg.create(name)
     assert s_full.init(g, p) == A.CFD_SUCCESS
     for step in range(4):
         _cavity_bc(f)
