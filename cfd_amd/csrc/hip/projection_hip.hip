@@ -1339,8 +1339,11 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             cg.tiles_y = (int)((ny - 1 + CCF_OY - 1) / CCF_OY);
             // 32-plane z runs: 1.155-1.18 vs 1.24-1.29 ms per iteration at
             // 512^3 against 128 (684 workgroups are 2.7 rounds of 256; 64:
-            // 1.16-1.24, 16: 1.20-1.21; profiles/r04_ccf_kc_*.jsonl)
-            cg.kc = 32;
+            // 1.16-1.24, 16: 1.20-1.21; profiles/r04_ccf_kc_*.jsonl). One
+            // device: 24 (r05, two boxes, every stable pair: 1.048-1.049 vs
+            // 1.059 ms, profiles/r05an_*, r05ao_ccf_kc_ab.jsonl); Z-slabs keep
+            // 32 -> 16, whose thin-slab rounds 24 would leave part-empty
+            cg.kc = (c->nranks == 1) ? 24 : 32;
             const char* ekc = getenv("CFD_HIP_CCF_KC");  // experiments
             if (ekc) cg.kc = std::max(1, atoi(ekc));
             const bool kc_fixed = getenv("CFD_HIP_CCF_KC_FIXED") != nullptr;
