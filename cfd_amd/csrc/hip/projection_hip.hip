@@ -1343,7 +1343,15 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             // device: 24 (r05, two boxes, every stable pair: 1.048-1.049 vs
             // 1.059 ms, profiles/r05an_*, r05ao_ccf_kc_ab.jsonl); Z-slabs keep
             // 32 -> 16, whose thin-slab rounds 24 would leave part-empty
-            cg.kc = (c->nranks == 1) ? 24 : 32;
+            cg.kc = 32;
+            if (c->nranks == 1) {
+                // 24 unless that leaves a last round of workgroups under a
+                // quarter full (e.g. 171 columns x 3 runs = 513 on 256 CUs)
+                const long long cus = std::max(1, c->grid_cap / 8);
+                const long long b24 = (long long)cg.tiles_x * cg.tiles_y * ((nint_k + 23) / 24);
+                const long long tail = b24 % cus;
+                if (b24 >= 2 * cus && (tail == 0 || tail * 4 >= cus)) cg.kc = 24;
+            }
             const char* ekc = getenv("CFD_HIP_CCF_KC");  // experiments
             if (ekc) cg.kc = std::max(1, atoi(ekc));
             const bool kc_fixed = getenv("CFD_HIP_CCF_KC_FIXED") != nullptr;
