@@ -1320,6 +1320,13 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             // (1024^2 x 512: 2.16 -> 2.05 ms per iteration against 64;
             // 32: 2.34, profiles/r04_rb2_kc.jsonl)
             r2.kc = 128;
+            // deep grids with many columns: three runs per column (1024^2 x
+            // 512: 170 planes, 2451 workgroups, 1.735-1.739 vs 1.748-1.751 ms
+            // per iteration against 128 in four same-box pairs on two boxes;
+            // 255: 1.78-1.80, 510: 2.02; profiles/r05as_rb2_kc_ab.jsonl)
+            if (nint_k >= 384 &&
+                3LL * r2.tiles_x * r2.tiles_y >= 8LL * std::max(1, c->grid_cap / 8))
+                r2.kc = (nint_k + 2) / 3;
             if (const char* e = getenv("CFD_HIP_RB2_KC")) r2.kc = std::max(1, atoi(e));
             while (r2.kc > 4 &&
                    (long long)r2.tiles_x * r2.tiles_y * ((nint_k + r2.kc - 1) / r2.kc) < 512)
