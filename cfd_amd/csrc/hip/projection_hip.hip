@@ -1344,21 +1344,15 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             cg.xofs = 0;
             cg.tiles_x = (int)((nx - 1 + CCF_OX - 1) / CCF_OX);
             cg.tiles_y = (int)((ny - 1 + CCF_OY - 1) / CCF_OY);
-            // 32-plane z runs: 1.155-1.18 vs 1.24-1.29 ms per iteration at
-            // 512^3 against 128 (684 workgroups are 2.7 rounds of 256; 64:
-            // 1.16-1.24, 16: 1.20-1.21; profiles/r04_ccf_kc_*.jsonl). One
-            // device: 24 (r05, two boxes, every stable pair: 1.048-1.049 vs
-            // 1.059 ms, profiles/r05an_*, r05ao_ccf_kc_ab.jsonl); Z-slabs keep
-            // 32 -> 16, whose thin-slab rounds 24 would leave part-empty
-            cg.kc = 32;
-            if (c->nranks == 1) {
-                // 24 unless that leaves a last round of workgroups under a
-                // quarter full (e.g. 171 columns x 3 runs = 513 on 256 CUs)
-                const long long cus = std::max(1, c->grid_cap / 8);
-                const long long b24 = (long long)cg.tiles_x * cg.tiles_y * ((nint_k + 23) / 24);
-                const long long tail = b24 % cus;
-                if (b24 >= 2 * cus && (tail == 0 || tail * 4 >= cus)) cg.kc = 24;
-            }
+            // z-run length: 24 planes on deep grids, 16 on thin ones (r05;
+            // r04 had 32). 512^3 on one device: 24 at 1.048-1.049 vs 32's
+            // 1.059 ms per iteration in every stable pair on two boxes (20 and
+            // 28 equal to 24, 40 slower; profiles/r05ao_ccf_kc_ab.jsonl). The
+            // rank-0 slab shapes of 2 / 4 / 8 ranks, 512^2 x 257 / 130 / 66:
+            // 16 at 0.600-0.604 / 0.316-0.319 / 0.171 ms against 24's 0.613-
+            // 0.615 / 0.317-0.318 / 0.169 and 32's 0.627-0.630 / 0.334-0.335 /
+            // 0.197 (profiles/r05at_ccf_kc_thin_ab.jsonl)
+            cg.kc = (nint_k > 300) ? 24 : 16;
             const char* ekc = getenv("CFD_HIP_CCF_KC");  // experiments
             if (ekc) cg.kc = std::max(1, atoi(ekc));
             const bool kc_fixed = getenv("CFD_HIP_CCF_KC_FIXED") != nullptr;
