@@ -711,8 +711,8 @@ def cg_variant_auto(n, world, case="cavity"):
       the north star's design. Shared-GPU rehearsals at 512^3 (all ranks on
       one device, profiles/r05_slab_rehearsal/): N = 2 124.7 vs 112.6 MLUPS,
       N = 4 81.0 vs 70.4; on the N = 8 slab shape (66 planes) the march's
-      compute is 0.181 vs 0.163 ms per iteration (profiles/r05e_kc.jsonl)
-      against one all-reduce saved.
+      compute is 0.171 vs 0.163 ms per iteration (16-plane runs,
+      profiles/r05at_ccf_kc_thin_ab.jsonl) against one all-reduce saved.
     The Taylor-Green case keeps the textbook CG its parity tests pin."""
     if case != "cavity":
         return 0
