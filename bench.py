@@ -106,6 +106,10 @@ def parse():
     ap.add_argument("--fixed-cg-iters", type=int, default=200,
                     help="fixed-iteration CG microbench per variant after the timed region "
                          "(SURVEY.md §8d config 3; 0: skip)")
+    ap.add_argument("--no-plugin-step", action="store_true",
+                    help="skip the host-buffer plugin-step measurement after the timed region")
+    ap.add_argument("--plugin-steps", type=int, default=3,
+                    help="host-buffer plugin steps per mode (the first is not averaged)")
     ap.add_argument("--no-compare-cg-variant", action="store_true",
                     help="skip the side measurement of the other CG variant after the "
                          "timed region")
@@ -218,7 +222,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    iters = [step() for _ in range(args.steps)]
+    iters, step_ms = [], []
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        iters.append(step())  # returns after the step's CG solve has drained
+        step_ms.append((time.perf_counter() - ts) * 1e3)
     ctx.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -230,6 +238,10 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt[0])
+    # effective shader clock of the march's own workgroups over the timed
+    # region (sampled launches, hip_proj_get_clock_sample), so the line
+    # says which clock its box ran at
+    clk_mhz, clk_wg = ctx.clock_sample()
 
     n_int = (n - 2) ** 3
     n_loc = (n - 2) ** 2 * (ctx.nz_local - 2)  # interior cells of this rank's slab
@@ -246,11 +258,15 @@ def main():
     credited_equiv = credited * args.steps / elapsed / 1e9
 
     kt = ctx.timing()
+    # the march's plain (+ first) and x-fold launches time apart (ABI 3);
+    # the roofline is on their sum, one launch per CG iteration
+    kt_all = dict(kt)
+    kt_all["cc_march"] = (kt["cc_fused"][0] + kt["cc_fold"][0], kt["cc_fused"][1] + kt["cc_fold"][1])
     sweeps = {}   # timer -> (kernel symbol, B/cell, avg ms, launches, achieved GB/s, total ms)
     sweep_set = sweep_kernels(args.sweep_rows, world > 1, args.sweep_variant, args.cg_variant,
                               ctx.nz_local - 2)
     for key, kname, bpc in sweep_set:
-        ms, cnt = kt[key]
+        ms, cnt = kt_all[key]
         avg = ms / cnt if cnt else None
         ach = bpc * n_loc / (avg * 1e-3) / 1e9 if cnt else None
         sweeps[key] = (kname, bpc, avg, cnt, ach, ms)
@@ -265,8 +281,8 @@ def main():
                               bpc_small * n_loc / (avg * 1e-3) / 1e9, small_ms)
     if small_n:  # one iteration = the solve's time / its iterations
         cg_iter_ms = small_ms / max(1, sum(iters))
-    elif args.cg_variant == 1 and "cc_fused" in sweeps:  # the march (+ the slab SpMV)
-        cg_iter_ms = (sweeps["cc_fused"][2] or 0.0) + (
+    elif args.cg_variant == 1 and "cc_march" in sweeps:  # the march (+ the slab SpMV)
+        cg_iter_ms = (sweeps["cc_march"][2] or 0.0) + (
             (sweeps["cc_spmv"][2] or 0.0) if "cc_spmv" in sweeps else 0.0)
     elif args.cg_variant == 1:  # one iteration = update + SpMV
         cg_iter_ms = (sweeps["cc_update"][2] or 0.0) + (sweeps["cc_spmv"][2] or 0.0)
@@ -288,13 +304,13 @@ def main():
         traffic_src = (prof["file"] + ": " + ("k_ccf<*, *, false> (launch-weighted)"
                                               if kname == "k_ccf<false, false, false>"
                                               else kname)) if bpl else None
-        names = {k: v[0] for k, v in sweeps.items()}
+        names = {k: v[0] for k, v in sweeps.items() if k != "cc_march"}
         tot = 0.0
         for key, (ms, cnt) in kt.items():
             if not cnt:
                 continue
             kn = names.get(key) or TIMER_KERNEL.get(key)
-            rec = prof_record(prof, kn) if kn else None
+            rec = prof_record(prof, kn, key) if kn else None
             if rec and "hbm_bytes_per_launch" in rec:
                 tot += rec["hbm_bytes_per_launch"] * cnt
                 measured_from.append(kn)
@@ -341,11 +357,16 @@ def main():
     # side measurement of the other CG variant (same grid, ranks and stepping
     # from the same initial state), after the timed region: per CG iteration,
     # since its iteration counts differ from the main run's by rounding
+    # The other variant times the SAME step as the main run's first timed
+    # one: a fresh context steps the warm-up steps untimed, then step
+    # warmup + 1 is timed (its CG iterations are that step's count), next to
+    # the main run's own wall time of that step
     other = None
     if not args.no_compare_cg_variant:
         ctx.close()
         ctx = make_ctx(1 - args.cg_variant)
-        step()
+        for _ in range(args.warmup):
+            step()
         ctx.synchronize()
         ctx.reset_timing()
         ctx.enable_timing(True)
@@ -364,14 +385,30 @@ def main():
         k2 = ctx.timing()
         per2 = lambda key: round(k2[key][0] / max(1, it2), 4) if k2[key][1] else None
         other = {"cg_variant": 1 - args.cg_variant, "step": args.warmup + 1,
+                 "timed": f"step {args.warmup + 1} of a fresh context after "
+                          f"{args.warmup} untimed steps (the main run's first timed step)",
                  "cg_iters": it2, "ms_step": round(e2 * 1e3, 3),
                  "ms_per_cg_iter_wall": round(e2 * 1e3 / max(1, it2), 4),
                  "kernel_ms_per_iter": {k: per2(k) for k in k2 if k2[k][1]},
-                 "main_ms_per_cg_iter_wall": round(elapsed * 1e3 / tot_iters, 4)}
+                 "main_same_step": {"cg_iters": iters[0], "ms_step": round(step_ms[0], 3),
+                                    "ms_per_cg_iter_wall": round(step_ms[0] / max(1, iters[0]),
+                                                                 4)},
+                 "main_ms_per_cg_iter_wall_all_steps": round(elapsed * 1e3 / tot_iters, 4)}
         if cos_rhs is not None:
             fixed200[f"cg_variant_{1 - args.cg_variant}"] = fixed_cg(
                 ctx, g, params, n_int, 1 - args.cg_variant, cos_rhs, args.fixed_cg_iters)
     del cos_rhs
+
+    # the reference caller's throughput: projection_hip_cg1 through
+    # solver_step on host buffers (solver_registry.c:438-458, as
+    # run_simulation_step drives it, simulation_api.c:185-202), full
+    # transfers and the resident dirty-faces mode, beside the HBM-resident
+    # step on the same steps; never `value`
+    plug = None
+    if world == 1 and not tg and not args.no_plugin_step:
+        ctx.close()
+        ctx = None
+        plug = plugin_step(n, g, params, make_ctx, args.plugin_steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
@@ -432,14 +469,24 @@ def main():
                               "achieved_GBps": round(v[4], 1) if v[4] else None}
                           for k, v in sweeps.items()},
             "ranks": ranks,
+            "ccf_launches": ccf_split(kt, n_loc, world) if args.cg_variant == 1 else None,
+            "clock": {"k_ccf_shader_MHz": round(clk_mhz, 1) if clk_wg else None,
+                      "sampled_workgroups": clk_wg,
+                      "how": ("wave 0 of every workgroup of 2 in 8 k_ccf launches stamps "
+                              "s_memtime / s_memrealtime at its start and end; MHz = 100 x "
+                              "sum d memtime / sum d memrealtime (rank 0)")},
+            "step_ms": [round(v, 2) for v in step_ms],
             "cg_variant": args.cg_variant,
+            "cg_variant_choice": cg_variant_choice(world, args),
             "cg_variant_compare": other,
+            "plugin_step": plug,
             "cg_fixed200": ({"iterations": args.fixed_cg_iters, "x0": "zero",
                              "early_exit": False, **fixed200} if fixed200 else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if comm is not None:
         comm.close()
     if world > 1:
@@ -644,7 +691,10 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
 _PC_OLD = os.environ.get("CFD_HIP_PC3", "1") == "0"
 TIMER_KERNEL = {"predictor": "k_pred2<false, 0>" if _PC_OLD else "k_pred3<false, 0>",
                 "corrector": "k_corr2<0>" if _PC_OLD else "k_corr3<0>",
-                "cg_setup": "k_cg_setup<true, false, true, false>"}
+                "cg_setup": "k_cg_setup<true, false, true, false>",
+                # one device: the march's plain (+ first) and fold launches
+                "cc_fused": "k_ccf<false, false, false>",
+                "cc_fold": "k_ccf<false, false, false>"}
 
 
 def sweep_kernels(rows, dist_, variant, cg_variant, planes=None):
@@ -656,14 +706,14 @@ def sweep_kernels(rows, dist_, variant, cg_variant, planes=None):
     if cg_variant == 1 and not dist_:
         # one z-march per iteration (ccf.hpp); the timer spans the plain and
         # the fold launches, so the byte count is their mean
-        return (("cc_fused", "k_ccf<false, false, false>", BYTES_CC_FUSED),)
+        return (("cc_march", "k_ccf<false, false, false>", BYTES_CC_FUSED),)
     if cg_variant == 1:
         # Z-slabs, fused form (r05): the edge planes' march (k_ccf<.., true>,
         # untimed, 2 planes), the r halo, the interior march with w and the
         # dots (the timer), then w = A r in registers on the two edge planes
         # completing the one reduction (k_cc2 without the w store): its bytes
         # per slab cell are 8 B x 2 / planes
-        return (("cc_fused", "k_ccf<false, false, false>", BYTES_CC_FUSED),
+        return (("cc_march", "k_ccf<false, false, false>", BYTES_CC_FUSED),
                 ("cc_spmv", f"k_cc2<{rows}, {d}, false, false>",
                  BYTES_CC_SPMV_NOW * 2.0 / planes if planes else BYTES_CC_SPMV_NOW))
     return (("cg_sweep_a", f"k_cgA<{rows}, false, {d}, {variant}, false>", BYTES_SWEEP_A),
@@ -672,6 +722,115 @@ def sweep_kernels(rows, dist_, variant, cg_variant, planes=None):
 
 
 BYTES_CG_TEXTBOOK = 58.0  # textbook CG per iteration: sweeps A + B (48) + the x fold / 4 (10)
+BYTES_CCF_PLAIN = 32.0    # k_ccf plain launch: read r_it, p_{it-1}; write p_it, r_{it+1}
+BYTES_CCF_FOLD = 64.0     # k_ccf fold launch: + read x, p_{it-3}, p_{it-2}; write x
+
+
+def ccf_split(kt, n_loc, world):
+    """The march's plain (+ first) and x-fold launches apart: average launch
+    time, count and algorithmic rate on their own bytes (32 / 64 B/cell). On
+    Z-slabs the timers hold the interior launch only."""
+    out = {}
+    for key, bpc in (("cc_fused", BYTES_CCF_PLAIN), ("cc_fold", BYTES_CCF_FOLD)):
+        ms, cnt = kt[key]
+        if not cnt:
+            out[key] = None
+            continue
+        avg = ms / cnt
+        gbps = bpc * n_loc / (avg * 1e-3) / 1e9
+        out[key] = {"launches": cnt, "avg_ms": round(avg, 4), "bytes_per_cell": bpc,
+                    "achieved_GBps": round(gbps, 1),
+                    "frac_of_8TBps": round(gbps / HBM_PEAK_GBPS, 4)}
+    out["note"] = ("cc_fused: the first and plain launches (32 B/cell; the first reads no "
+                   "p_{it-1}), cc_fold: every 4th, which also folds x" +
+                   ("; Z-slabs: the interior launch" if world > 1 else ""))
+    return out
+
+
+def plugin_step(n, g, params, make_ctx, nsteps):
+    """projection_hip_cg1 through the reference interface on host buffers:
+    Registry().create + solver_init + solver_step on a flow_field, from rest
+    (the cavity BCs once, as the fixture's run), `nsteps` steps with full
+    transfers (u, v, w, p up and down every step) and with the resident
+    dirty-faces mode (CFD_HIP_DIRTY_FACES: only the boundary shell moves),
+    beside the HBM-resident step_device of the same steps. Steps 2.. are
+    averaged (step 1 of the resident mode uploads in full). pcie_share =
+    1 - resident / host-buffer time of the same steps."""
+    import ctypes as C
+
+    from cfd_amd import _abi as A
+    from cfd_amd import _native, api
+
+    lib = _native.hip()
+    out = {"solver": "projection_hip_cg1", "steps": nsteps, "averaged_steps": f"2..{nsteps}"}
+    f = api.FlowField(n, n, n)
+    reg = api.Registry()
+
+    def reset_field():
+        for k in ("u", "v", "w", "p", "T"):
+            getattr(f, k)[...] = 0.0
+        f.rho[...] = 1.0
+        api.cavity_bc(f, 1.0)
+
+    saved = os.environ.get("CFD_HIP_DIRTY_FACES")
+    try:
+        for mode, env in (("full", None), ("dirty_faces", "1000")):
+            if env is None:
+                os.environ.pop("CFD_HIP_DIRTY_FACES", None)
+            else:
+                os.environ["CFD_HIP_DIRTY_FACES"] = env
+            reset_field()
+            solver = reg.create("projection_hip_cg1")
+            try:
+                if solver.init(g, params) != A.CFD_SUCCESS:
+                    raise RuntimeError("plugin init: " + _native.last_error())
+                hctx = C.cast(solver._ptr.contents.context, C.POINTER(C.c_void_p))[0]
+                ms, its = [], []
+                for _ in range(nsteps):
+                    st = A.SolverStats()
+                    t0 = time.perf_counter()
+                    s = solver.step(f, g, params, st)
+                    ms.append((time.perf_counter() - t0) * 1e3)
+                    if s != A.CFD_SUCCESS:
+                        raise RuntimeError(f"plugin step {s}: {_native.last_error()}")
+                    ps = A.PoissonStats()
+                    lib.hip_proj_get_poisson_stats(hctx, C.byref(ps))
+                    its.append(ps.iterations)
+            finally:
+                solver.close()
+            out[mode] = {"ms_per_step": [round(v, 2) for v in ms], "cg_iters": its}
+    finally:
+        if saved is None:
+            os.environ.pop("CFD_HIP_DIRTY_FACES", None)
+        else:
+            os.environ["CFD_HIP_DIRTY_FACES"] = saved
+    del f
+    c = make_ctx(1)
+    try:
+        ms, its = [], []
+        for _ in range(nsteps):
+            t0 = time.perf_counter()
+            if c.step_device(g, params) != A.CFD_SUCCESS:
+                raise RuntimeError("resident step: " + _native.last_error())
+            its.append(c.poisson_stats().iterations)
+            c.synchronize()
+            ms.append((time.perf_counter() - t0) * 1e3)
+    finally:
+        c.close()
+    out["resident"] = {"ms_per_step": [round(v, 2) for v in ms], "cg_iters": its}
+    mean = lambda v: sum(v[1:]) / max(1, len(v) - 1)
+    res = mean(out["resident"]["ms_per_step"])
+    cells = (n - 2) ** 3
+    for mode in ("full", "dirty_faces", "resident"):
+        m = mean(out[mode]["ms_per_step"])
+        out[mode]["ms_mean"] = round(m, 2)
+        out[mode]["MLUPS"] = round(cells / (m * 1e-3) / 1e6, 2)
+    out["ms_full"] = out["full"]["ms_mean"]
+    out["ms_dirty_faces"] = out["dirty_faces"]["ms_mean"]
+    out["ms_resident"] = round(res, 2)
+    out["pcie_share"] = {"full": round(1.0 - res / out["ms_full"], 4),
+                         "dirty_faces": round(1.0 - res / out["ms_dirty_faces"], 4)}
+    return out
 
 
 def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
@@ -700,32 +859,70 @@ def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
     return out
 
 
+def slab_budget():
+    """The newest committed N-rank per-iteration budget
+    (profiles/*_slab_budget.json, written by tools/slab_budget.py from
+    one-GPU timings of each piece of a slab iteration), or None."""
+    for path in sorted((ROOT / "profiles").glob("*_slab_budget.json"), reverse=True):
+        try:
+            d = json.loads(path.read_text())
+        except (OSError, ValueError):
+            continue
+        if isinstance(d.get("projected_ms_per_iter"), dict):
+            d["file"] = path.name
+            return d
+    return None
+
+
 def cg_variant_auto(n, world, case="cavity"):
-    """The bench's CG variant: the single-reduction CG (projection_hip_cg1) for
-    the cavity wherever it is measured faster than textbook CG:
-    - one GPU at n >= 512: the fused march k_ccf (1.07-1.20 vs 1.31 ms per
-      iteration at 512^3, box-dependent; DESIGN.md section 3);
-    - Z-slabs (N > 1): the r05 fused slab form (edge planes, the r halo on the
-      side stream over the interior march, which also forms w and the dots,
-      then k_cc2 on the edge planes only) with ONE all-reduce per iteration,
-      the north star's design. Shared-GPU rehearsals at 512^3 (all ranks on
-      one device, profiles/r05_slab_rehearsal/): N = 2 124.7 vs 112.6 MLUPS,
-      N = 4 81.0 vs 70.4; on the N = 8 slab shape (66 planes) the march's
-      compute is 0.171 vs 0.163 ms per iteration (16-plane runs,
-      profiles/r05at_ccf_kc_thin_ab.jsonl) against one all-reduce saved.
+    """The bench's CG variant for the cavity:
+    - one GPU at n >= 512: the single-reduction march k_ccf (1.05-1.17 vs
+      1.31-1.35 ms per iteration at 512^3 on the same box, DESIGN.md
+      section 3);
+    - Z-slabs (N > 1): the variant whose projected per-iteration time at this
+      N is lower in the committed slab budget (tools/slab_budget.py: every
+      piece of one rank's iteration -- edge launch, interior march, edge
+      SpMV, plane exchange, the dot all-reduces -- timed on one GPU at that
+      N's slab shape); with no budget for this N,
+      textbook CG, the reference's loop.
     The Taylor-Green case keeps the textbook CG its parity tests pin."""
     if case != "cavity":
         return 0
-    return 1 if (world > 1 or n >= 512) else 0
+    if world == 1:
+        return 1 if n >= 512 else 0
+    b = slab_budget()
+    proj = (b or {}).get("projected_ms_per_iter", {}).get(str(world)) if n == 512 else None
+    if not proj or "cg0" not in proj or "cg1" not in proj:
+        return 0
+    return 1 if proj["cg1"] < proj["cg0"] else 0
 
 
-def prof_record(prof, kname):
-    """PMC record of a timer's kernel. The one-device single-reduction timer
+def cg_variant_choice(world, args):
+    """Why this run's CG variant was chosen (the bench line's record)."""
+    if args.case != "cavity":
+        return {"rule": "Taylor-Green: textbook CG"}
+    if world == 1:
+        return {"rule": "one GPU at n >= 512: single-reduction march (k_ccf)"}
+    b = slab_budget()
+    proj = (b or {}).get("projected_ms_per_iter", {}).get(str(world))
+    return {"rule": "N > 1: the lower projected per-iteration time of the committed slab "
+                    "budget at this N (textbook CG without one)",
+            "budget_file": b["file"] if b else None, "projected_ms_per_iter": proj,
+            "measured_on": (b or {}).get("measured_on")}
+
+
+def prof_record(prof, kname, key=None):
+    """PMC record of a timer's kernel. The one-device single-reduction march
     spans k_ccf's first, plain and fold launches (k_ccf<*, *, false>): their
-    bytes per launch averaged over the profiled launch counts."""
+    bytes per launch averaged over the profiled launch counts; with the timer
+    key, "cc_fused" averages the first and plain launches and "cc_fold" is
+    the fold launch's record."""
     if kname == "k_ccf<false, false, false>":
+        want = {"cc_fused": ("k_ccf<true, false, false>", "k_ccf<false, false, false>"),
+                "cc_fold": ("k_ccf<false, true, false>",)}.get(key)
         recs = [v for k, v in prof["kernels"].items()
                 if k.startswith("k_ccf<") and k.endswith(", false>")
+                and (want is None or k in want)
                 and "hbm_bytes_per_launch" in v and v.get("calls")]
         n = sum(v["calls"] for v in recs)
         if n:

@@ -41,9 +41,9 @@ HIP_POISSON_JACOBI = 2
 HIP_FIELD_U, HIP_FIELD_V, HIP_FIELD_W, HIP_FIELD_P, HIP_FIELD_T, HIP_FIELD_RHO = range(6)
 KERNEL_TIMERS = ["predictor", "cg_setup", "cg_sweep_a", "cg_sweep_b", "corrector",
                  "relax", "residual", "energy", "rk_stage", "cg_sweep_bx", "cc_update",
-                 "cc_spmv", "halo", "allreduce", "cg_small", "relax2", "cc_fused"]
+                 "cc_spmv", "halo", "allreduce", "cg_small", "relax2", "cc_fused", "cc_fold"]
 HIP_KT_COUNT = len(KERNEL_TIMERS)
-HIP_PROJ_ABI_VERSION = 2  # projection_hip.h
+HIP_PROJ_ABI_VERSION = 3  # projection_hip.h
 
 # oracle_poisson_kind_t
 ORACLE_POISSON_CG = 0

@@ -189,6 +189,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_reset_timing", None, V)
     _sig(lib, "hip_proj_get_timing", None, V, A.c_double_p, P(C.c_longlong))
     _sig(lib, "hip_proj_get_timing_n", C.c_int, V, A.c_double_p, P(C.c_longlong), C.c_int)
+    _sig(lib, "hip_proj_get_clock_sample", C.c_int, V, P(C.c_double), P(C.c_longlong))
     _sig(lib, "hip_proj_abi_version", C.c_int)
     _sig(lib, "hip_proj_build_id", C.c_char_p)
     _sig(lib, "hip_proj_synchronize", C.c_int, V)
@@ -216,6 +217,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_comm_rank", C.c_int, V)
     _sig(lib, "hip_proj_comm_size", C.c_int, V)
     _sig(lib, "hip_proj_comm_device_allreduce", C.c_int, V)
+    _sig(lib, "hip_proj_comm_mailbox_bench", C.c_int, V, C.c_int, C.c_int, P(C.c_double))
     _sig(lib, "hip_proj_create_slab", V, C.c_size_t, C.c_size_t, C.c_size_t, V,
          P(A.HipProjConfig))
     _sig(lib, "hip_proj_slab_info", C.c_int, V, P(C.c_size_t), P(C.c_size_t), P(C.c_int),

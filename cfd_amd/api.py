@@ -370,6 +370,17 @@ class SlabComm:
     def device_allreduce(self) -> bool:
         return bool(_native.hip().hip_proj_comm_device_allreduce(self._h))
 
+    def allreduce_bench(self, iters: int, mode: int) -> float:
+        """Collective: microseconds per two-value CG dot all-reduce
+        (hip_proj_comm_mailbox_bench; mode 0 mailbox round trip inside one
+        kernel, 1 one launch + mailbox per all-reduce, 2 ncclAllReduce +
+        a check kernel)."""
+        us = C.c_double(0.0)
+        st = _native.hip().hip_proj_comm_mailbox_bench(self._h, iters, mode, C.byref(us))
+        if st != A.CFD_SUCCESS:
+            raise CfdError(st, "allreduce bench: " + _native.last_error())
+        return us.value
+
     def close(self):
         if getattr(self, "_h", None):
             _native.hip().hip_proj_comm_destroy(self._h)
@@ -566,6 +577,13 @@ class HipProjection:
 
     def reset_timing(self):
         self._lib().hip_proj_reset_timing(self._ctx)
+
+    def clock_sample(self):
+        """(MHz, workgroups): the effective shader clock of the sampled k_ccf
+        workgroups since reset_timing (hip_proj_get_clock_sample)."""
+        mhz, n = C.c_double(0.0), C.c_longlong(0)
+        self._lib().hip_proj_get_clock_sample(self._ctx, C.byref(mhz), C.byref(n))
+        return mhz.value, n.value
 
     def timing(self):
         ms = (C.c_double * A.HIP_KT_COUNT)()

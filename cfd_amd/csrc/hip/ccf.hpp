@@ -115,11 +115,21 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     SGeo g, Lap Lp, const double* __restrict__ R0, double* __restrict__ R1,
     const double* __restrict__ Po, double* __restrict__ Pn, PPrev pv, double* __restrict__ x,
     CgState* st, double* partials, unsigned* counter, int it, int xmap, int dist, double* dsum,
-    Mbox* mb) {
+    Mbox* mb, unsigned long long* clk) {
     // (a fold step reads p_{it-1} from the po ring, which FIRST never loads)
     static_assert(!(FIRST && FOLD), "k_ccf: no fold in the first iteration");
     __shared__ CcfLds L;
     if (CCF_DIAG == 0 && st->done) return;
+    // clock sample (clk != nullptr on one launch in eight while the context
+    // times its kernels, hip_proj_get_clock_sample): wave 0 stamps the shader
+    // clock (s_memtime) and the 100 MHz constant clock (s_memrealtime) at the
+    // workgroup's start and end; uniform branch, no stamp in other launches
+    unsigned long long clk_t0 = 0, clk_r0 = 0;
+    if (clk != nullptr && threadIdx.x < 64) {
+        clk_t0 = __builtin_amdgcn_s_memtime();
+        clk_r0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the stamps are back
+    }
     const double a = st->alpha[it % CG_XFOLD];
     const double ma = -a;
     const double beta = FIRST ? 0.0 : st->beta;
@@ -360,6 +370,16 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     if (n < nsteps) step(IntC<0>{}, q0 + n);
     if (n + 1 < nsteps) step(IntC<1>{}, q0 + n + 1);
     if (n + 2 < nsteps) step(IntC<2>{}, q0 + n + 2);
+    if (clk != nullptr && threadIdx.x < 64) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (threadIdx.x == 0) {  // vector atomics (no-return adds)
+            atomicAdd(&clk[0], t1 - clk_t0);
+            atomicAdd(&clk[1], r1 - clk_r0);
+            atomicAdd(&clk[2], 1ull);
+        }
+    }
     if constexpr (NOC) return;  // k_cc2 reduces
     // ---- one reduction: (gamma, delta) of iteration it + 1 ----
     accg = wave_sum(accg);

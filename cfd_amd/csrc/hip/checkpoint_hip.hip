@@ -198,6 +198,7 @@ cfd_status_t device_crcs(hip_proj_ctx* c, const double* const* fs, int nf, uint3
 extern "C" {
 
 cfd_status_t hip_proj_field_crc32(hip_proj_ctx_t* c, int field_id, uint32_t* crc) {
+    GroupHostLock hl_(c);
     if (!c || !crc) return CFD_ERROR_INVALID;
     const double* f = field_ptr(c, field_id);
     if (!f) return CFD_ERROR_INVALID;
@@ -212,6 +213,7 @@ cfd_status_t hip_proj_checkpoint_write(hip_proj_ctx_t* c, const char* path, cons
                                        const ns_solver_params_t* params, double current_time,
                                        const char* solver_name, const char* run_prefix,
                                        const char* output_base_dir) {
+    GroupHostLock hl_(c);
     if (!c || !path || !g || !params || !solver_name) {
         set_err(CFD_ERROR_INVALID, "hip_proj_checkpoint_write: NULL argument");
         return CFD_ERROR_INVALID;
@@ -308,6 +310,7 @@ cfd_status_t hip_proj_checkpoint_read(hip_proj_ctx_t* c, const char* path, grid*
                                       char* out_solver_name, size_t solver_name_cap,
                                       char* out_run_prefix, size_t run_prefix_cap,
                                       char* out_output_base_dir, size_t output_base_dir_cap) {
+    GroupHostLock hl_(c);
     if (out_grid) *out_grid = nullptr;
     if (!c || !path || !out_params) {
         set_err(CFD_ERROR_INVALID, "hip_proj_checkpoint_read: NULL argument");

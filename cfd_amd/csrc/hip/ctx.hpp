@@ -87,6 +87,7 @@ struct hip_proj_ctx {
     size_t nzg = 0;    // global nz
     size_t kofs = 0;   // global index of local plane 0
     double* dsum = nullptr;            // [0] local dot total, [1] all-reduced
+    unsigned long long* clk = nullptr;  // k_ccf clock sample: sum d memtime, d memrealtime, count
     hipStream_t hstream = nullptr;     // side stream: halo of r overlaps the (r,r) all-reduce
     hipEvent_t ev_b = nullptr, ev_h = nullptr;
     unsigned long long* redg = nullptr;  // all-reduced red[]
@@ -170,6 +171,12 @@ struct hip_proj_ctx {
         int rb2_xmap = 0;         // CFD_HIP_RB2_XMAP (experiments)
         bool rb2_log = false;     // CFD_HIP_RB2_LOG (diagnostics)
         int rb2 = 1;              // CFD_HIP_RB2: 1 certified fast, 2 exact, 0 k_rb1
+        int ccf_xmap = 0;         // CFD_HIP_CCF_XMAP: k_ccf tile order (experiments)
+        bool cgb_rev = true;      // CFD_HIP_CGB_REV=0: sweep B marches upwards
+        bool rb1_pf = true;       // CFD_HIP_RB1_PF=0: k_rb1 end-of-step loads
+        bool rb1_alt = true;      // CFD_HIP_RB1_ALT=0: every k_rb1 sweep upwards
+        bool rb1_fold = true;     // CFD_HIP_RB1_FOLD=0: separate k_rx_shell launch
+        bool rk_pair = true;      // CFD_HIP_RK_PAIR=0: per-cell RK4 stage
     } env;
     // timing
     int timing = 0;

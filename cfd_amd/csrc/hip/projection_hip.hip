@@ -34,8 +34,7 @@ static void launch_cgB_t(hip_proj_ctx* c, const SGeo& sg, const Lap& L, const BA
     // planes sweep A touched last, in the Infinity Cache; 512^3 sweep B
     // 0.551 -> 0.539 ms, CG iteration 1.355 -> 1.335 ms, profiles/r03_rev.jsonl);
     // CFD_HIP_CGB_REV=0 restores the upward march
-    static const bool rev = !(getenv("CFD_HIP_CGB_REV") && atoi(getenv("CFD_HIP_CGB_REV")) == 0);
-    if (!DIST && rev && c->geo.sz && sg.kmode == 0) {
+    if (!DIST && c->env.cgb_rev && c->geo.sz && sg.kmode == 0) {
         hipExtLaunchKernelGGL((k_cgB<TY, DIST, FL, true>), dim3(nb), dim3(64 * TY), 0, c->stream,
                               c->ta, c->tb, 0, sg, L, a.p, a.r, c->st, c->partials, c->counter,
                               it, c->dsum, mbox(c));
@@ -182,10 +181,13 @@ static double* ccf_r1(hip_proj_ctx* c, int it) { return (it & 1) ? c->r : c->r2;
 template <bool FIRST, bool FOLD, bool NOC>
 static void launch_ccf_t(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
                          const double* po, const PPrev& pv, double* x, int it, int xmap) {
+    // clock sample on one launch in eight while timing (iterations 5 and 7
+    // mod 8: a plain and a fold launch)
+    unsigned long long* clk = (c->timing && c->clk && (it & 5) == 5) ? c->clk : nullptr;
     hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD, NOC>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
                           dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, ccf_r0(c, it),
                           ccf_r1(c, it), po, pn, pv, x, c->st, c->partials, c->counter, it, xmap,
-                          dist(c) ? 1 : 0, c->dsum, mbox(c));
+                          dist(c) ? 1 : 0, c->dsum, mbox(c), clk);
 }
 
 template <bool NOC>
@@ -203,7 +205,7 @@ static void launch_ccf_n(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* p
 // interior planes in the fused form)
 static void launch_ccf(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
                        const double* po, const PPrev& pv, double* x, int it, bool noc) {
-    static const int xmap = getenv("CFD_HIP_CCF_XMAP") ? atoi(getenv("CFD_HIP_CCF_XMAP")) : 0;
+    const int xmap = c->env.ccf_xmap;
     if (noc) launch_ccf_n<true>(c, g, L, pn, po, pv, x, it, xmap);
     else launch_ccf_n<false>(c, g, L, pn, po, pv, x, it, xmap);
 }
@@ -333,8 +335,12 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
         double* pold = P[(it + CG_XFOLD - 1) % CG_XFOLD];
         PPrev pv;
         for (int q = 0; q < CG_XFOLD - 1; ++q) pv.q[q] = P[(it + 1 + q) % CG_XFOLD];
+        // the fold launches (x += the four pending alpha p, every 4th) time
+        // apart from the plain ones
+        const int kcf = (it > 0 && (it % CG_XFOLD) == CG_XFOLD - 1) ? HIP_KT_CC_FOLD
+                                                                     : HIP_KT_CC_FUSED;
         if (ccf && !D) {
-            timed(c, HIP_KT_CC_FUSED,
+            timed(c, kcf,
                   [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it, false); }, it);
             return CFD_SUCCESS;
         }
@@ -358,7 +364,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                     return c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false);
                 }, it));
                 HIP_TRY(hipEventRecord(c->ev_h, c->hstream));
-                timed(c, HIP_KT_CC_FUSED,
+                timed(c, kcf,
                       [&] { launch_ccf(c, fused ? c->cc_int_red : c->cc_int, L, pnew, pold, pv,
                                        x, it, !fused); }, it);
                 HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_h, 0));
@@ -366,7 +372,7 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
                     launch_cc2(c, L, it, false, r1, false, fused ? &c->cc2_edge : nullptr);
                 }, it);
             } else {
-                timed(c, HIP_KT_CC_FUSED,
+                timed(c, kcf,
                       [&] { launch_ccf(c, c->ccgeo, L, pnew, pold, pv, x, it, true); }, it);
                 ST_TRY(timed_span(c, c->stream, HIP_KT_HALO, [&] { return halo(c, {r1}); }, it));
                 timed(c, HIP_KT_CC_SPMV, [&] { launch_cc2(c, L, it, false, r1, false); }, it);
@@ -520,8 +526,7 @@ static void rb1_sweep_single(hip_proj_ctx* c, const RelaxCoef& rc, const double*
     const unsigned nb1 = (unsigned)(c->rgeo.tiles_x * c->rgeo.tiles_y * c->rgeo.tiles_z);
     // register-ring prefetch (default); CFD_HIP_RB1_PF=0 selects the
     // end-of-step loads (experiments)
-    static const bool rb1_pf = !(getenv("CFD_HIP_RB1_PF") &&
-                                 atoi(getenv("CFD_HIP_RB1_PF")) == 0);
+    const bool rb1_pf = c->env.rb1_pf;
     // memory hints of k_rb1 / k_rb1m (SW_* bits): FLR = 13, NT stores
     // of Y and plain rhs loads (r03: the NT rhs loads of 15 made the
     // neighbouring tiles re-fetch the rhs halo rows; 512^3 0.744 ->
@@ -531,9 +536,7 @@ static void rb1_sweep_single(hip_proj_ctx* c, const RelaxCoef& rc, const double*
     // the planes the previous one wrote last, in the Infinity Cache;
     // bitwise either way (kernels.hpp rb1_body). CFD_HIP_RB1_ALT=0:
     // every iteration upwards
-    static const bool rb1_alt = !(getenv("CFD_HIP_RB1_ALT") &&
-                                  atoi(getenv("CFD_HIP_RB1_ALT")) == 0);
-    const bool rev = rb1_alt && rb1_pf && (it & 1);
+    const bool rev = c->env.rb1_alt && rb1_pf && (it & 1);
 #define RB1_LAUNCH(TCV, PFV)                                                                   \
     hipExtLaunchKernelGGL((k_rb1<FLR, TCV, PFV>), dim3(nb1), dim3(1024), 0, c->stream, c->ta, \
                           c->tb, 0, c->rgeo, rc, xi, xo, c->rhs, st, c->partials,            \
@@ -813,9 +816,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
                         c->cfg.relax_two_pass == 0;
     // k_rb1 writes the iteration's Neumann shell itself (no k_rx_shell);
     // CFD_HIP_RB1_FOLD=0 keeps the separate shell launch (A/B)
-    static const bool fold_env = !(getenv("CFD_HIP_RB1_FOLD") &&
-                                   atoi(getenv("CFD_HIP_RB1_FOLD")) == 0);
-    const bool neu_fold = single && fold_env && c->poisson_bc == HIP_POISSON_BC_NEUMANN;
+    const bool neu_fold = single && c->env.rb1_fold && c->poisson_bc == HIP_POISSON_BC_NEUMANN;
     // two iterations per sweep on one device (rb2.hpp): CFD_HIP_RB2 = 1 (the
     // default: certified fast arithmetic), 2 (the reference's arithmetic
     // throughout), 0 (one iteration per sweep, k_rb1)
@@ -1160,6 +1161,7 @@ static void free_ctx(hip_proj_ctx* c) {
     if (c->red) hipFree(c->red);
     if (c->redg) hipFree(c->redg);
     if (c->dsum) hipFree(c->dsum);
+    if (c->clk) hipFree(c->clk);
     if (c->h_state) hipHostFree(c->h_state);
     if (c->h_red) hipHostFree(c->h_red);
     if (c->h_src) hipHostFree(c->h_src);
@@ -1197,6 +1199,12 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         c->env.rb2_xmap = ienv("CFD_HIP_RB2_XMAP", 0);
         c->env.rb2_log = getenv("CFD_HIP_RB2_LOG") != nullptr;
         c->env.rb2 = ienv("CFD_HIP_RB2", 1);
+        c->env.ccf_xmap = ienv("CFD_HIP_CCF_XMAP", 0);
+        c->env.cgb_rev = ienv("CFD_HIP_CGB_REV", 1) != 0;
+        c->env.rb1_pf = ienv("CFD_HIP_RB1_PF", 1) != 0;
+        c->env.rb1_alt = ienv("CFD_HIP_RB1_ALT", 1) != 0;
+        c->env.rb1_fold = ienv("CFD_HIP_RB1_FOLD", 1) != 0;
+        c->env.rk_pair = ienv("CFD_HIP_RK_PAIR", 1) != 0;
     }
     c->nx = nx;
     c->ny = ny;
@@ -1543,6 +1551,8 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     HIP_TRY(hipMemsetAsync(c->counter, 0, 64, c->stream));
     HIP_TRY(hipMalloc((void**)&c->red, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMalloc((void**)&c->redg, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&c->clk, 4 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(c->clk, 0, 4 * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMalloc((void**)&c->dsum, 4 * sizeof(double)));
     HIP_TRY(hipMemsetAsync(c->dsum, 0, 4 * sizeof(double), c->stream));
     HIP_TRY(hipHostMalloc((void**)&c->h_state, 3 * sizeof(CgState), hipHostMallocDefault));
@@ -1652,7 +1662,10 @@ cfd_status_t hip_proj_slab_info(const hip_proj_ctx_t* c, size_t* k_offset, size_
     return CFD_SUCCESS;
 }
 
-void hip_proj_destroy(hip_proj_ctx_t* ctx) { free_ctx(ctx); }
+void hip_proj_destroy(hip_proj_ctx_t* ctx) {
+    GroupHostLock hl_(ctx);  // holds the group, not the context: safe across the free
+    free_ctx(ctx);
+}
 
 size_t hip_proj_device_bytes(const hip_proj_ctx_t* ctx) { return ctx ? ctx->bytes : 0; }
 size_t hip_proj_row_pitch(const hip_proj_ctx_t* ctx) { return ctx ? (size_t)ctx->px : 0; }
@@ -1844,6 +1857,24 @@ void hip_proj_reset_timing(hip_proj_ctx_t* c) {
         c->kt_ms[k] = 0;
         c->kt_n[k] = 0;
     }
+    if (c->clk) {
+        hipMemsetAsync(c->clk, 0, 4 * sizeof(unsigned long long), c->stream);
+        hipStreamSynchronize(c->stream);
+    }
+}
+
+cfd_status_t hip_proj_get_clock_sample(hip_proj_ctx_t* c, double* mhz, long long* workgroups) {
+    GroupHostLock hl_(c);
+    if (!c) return CFD_ERROR_INVALID;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    if (c->clk) {
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(h, c->clk, sizeof(h), hipMemcpyDeviceToHost));
+    }
+    if (mhz) *mhz = h[1] ? 100.0 * (double)h[0] / (double)h[1] : 0.0;
+    if (workgroups) *workgroups = (long long)h[2];
+    return CFD_SUCCESS;
 }
 
 int hip_proj_get_timing_n(hip_proj_ctx_t* c, double* total_ms, long long* launches,
@@ -1861,7 +1892,7 @@ int hip_proj_get_timing_n(hip_proj_ctx_t* c, double* total_ms, long long* launch
 }
 
 void hip_proj_get_timing(hip_proj_ctx_t* c, double* total_ms, long long* launches) {
-    (void)hip_proj_get_timing_n(c, total_ms, launches, HIP_KT_COUNT_V1);
+    (void)hip_proj_get_timing_n(c, total_ms, launches, HIP_KT_COUNT_LEGACY);
 }
 
 int hip_proj_abi_version(void) { return HIP_PROJ_ABI_VERSION; }

@@ -37,7 +37,7 @@ template <int S>
 static void launch_stage(hip_proj_ctx* c, bool buoy, const RkCoef& rc, const Fld4& cur,
                          const Fld4& q0, const Fld4& acc, const Fld4& out) {
     // x-pair stage kernel (default); CFD_HIP_RK_PAIR=0 selects the per-cell one
-    static const bool pair = !(getenv("CFD_HIP_RK_PAIR") && atoi(getenv("CFD_HIP_RK_PAIR")) == 0);
+    const bool pair = c->env.rk_pair;
     if (pair) {
         const dim3 g2((unsigned)((c->nx + 127) / 128), (unsigned)((c->ny + 3) / 4),
                       (unsigned)c->nz);

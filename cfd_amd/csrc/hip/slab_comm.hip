@@ -516,3 +516,102 @@ int hip_proj_comm_device_allreduce(const hip_proj_comm_t* c) {
 int hip_proj_comm_size(const hip_proj_comm_t* c) { return c && c->impl ? c->impl->size : 0; }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// All-reduce microbenchmark (hip_proj_comm_mailbox_bench): the per-iteration
+// price of the CG dot exchange, the piece of the N-rank budget (DESIGN.md
+// section 5) that one GPU cannot time. Rank r contributes (r + 1 + i, 1) in
+// all-reduce i; every result is checked against n (n + 1) / 2 + n i and n.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void k_mbox_bench(cfdhip::Mbox* mb, int iters, int base, int* bad) {
+    if (threadIdx.x != 0) return;
+    const int n = mb->n, me = mb->rank;
+    for (int i = 0; i < iters; ++i) {
+        double a = 0.0, b = 0.0;
+        if (!cfdhip::mbox_allreduce2(mb, (double)(me + 1 + base + i), 1.0, &a, &b)) {
+            *bad = 2;  // a peer did not arrive within the mailbox's bound
+            return;
+        }
+        const double ea = 0.5 * n * (n + 1) + (double)n * (double)(base + i);
+        if (a != ea || b != (double)n) *bad = 1;
+    }
+}
+
+__global__ void k_bench_set(double* v, int rank, int i) {
+    if (threadIdx.x == 0) {
+        v[0] = (double)(rank + 1 + i);
+        v[1] = 1.0;
+    }
+}
+
+__global__ void k_bench_check(const double* s, int n, int i, int* bad) {
+    if (threadIdx.x == 0) {
+        const double ea = 0.5 * n * (n + 1) + (double)n * (double)i;
+        if (s[0] != ea || s[1] != (double)n) *bad = 1;
+    }
+}
+}  // namespace
+
+extern "C" cfd_status_t hip_proj_comm_mailbox_bench(hip_proj_comm_t* comm, int iters, int mode,
+                                                    double* us) {
+    if (us) *us = 0.0;
+    if (!comm || !comm->impl || iters <= 0 || mode < 0 || mode > 2 || !us)
+        return fail(CFD_ERROR_INVALID, "mailbox bench: bad arguments", nullptr);
+    SlabComm* c = comm->impl;
+    if (c->host_group())
+        return fail(CFD_ERROR_UNSUPPORTED, "mailbox bench: RCCL communicators only", nullptr);
+    cfdhip::Mbox* mb = c->device_mailbox();
+    if (mode < 2 && !mb)
+        return fail(CFD_ERROR_UNSUPPORTED, "mailbox bench: no device mailbox", nullptr);
+    HIPC(hipSetDevice(c->device));
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    double* d = nullptr;
+    int* bad = nullptr;
+    cfd_status_t st = CFD_SUCCESS;
+    float ms = 0.f;
+    int hbad = 0;
+    auto run = [&]() -> cfd_status_t {
+        HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIPC(hipEventCreate(&e0));
+        HIPC(hipEventCreate(&e1));
+        HIPC(hipMalloc((void**)&d, 8 * sizeof(double)));
+        HIPC(hipMalloc((void**)&bad, sizeof(int)));
+        HIPC(hipMemsetAsync(bad, 0, sizeof(int), s));
+        HIPC(hipMemsetAsync(d, 0, 8 * sizeof(double), s));
+        // start together: one all-reduce over RCCL first (ranks meet there)
+        cfd_status_t r = c->allreduce_sum(s, d, d + 4, 2);
+        if (r != CFD_SUCCESS) return r;
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipEventRecord(e0, s));
+        if (mode == 0) {
+            hipLaunchKernelGGL(k_mbox_bench, dim3(1), dim3(64), 0, s, mb, iters, 0, bad);
+        } else if (mode == 1) {
+            for (int i = 0; i < iters; ++i)
+                hipLaunchKernelGGL(k_mbox_bench, dim3(1), dim3(64), 0, s, mb, 1, i, bad);
+        } else {
+            for (int i = 0; i < iters; ++i) {
+                hipLaunchKernelGGL(k_bench_set, dim3(1), dim3(64), 0, s, d, c->rank, i);
+                if ((r = c->allreduce_sum(s, d, d + 2, 2)) != CFD_SUCCESS) return r;
+                hipLaunchKernelGGL(k_bench_check, dim3(1), dim3(64), 0, s, d + 2, c->size, i, bad);
+            }
+        }
+        HIPC(hipGetLastError());
+        HIPC(hipEventRecord(e1, s));
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipEventElapsedTime(&ms, e0, e1));
+        HIPC(hipMemcpy(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost));
+        return CFD_SUCCESS;
+    };
+    st = run();
+    if (bad) hipFree(bad);
+    if (d) hipFree(d);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    if (s) hipStreamDestroy(s);
+    if (st != CFD_SUCCESS) return st;
+    if (hbad) return fail(CFD_ERROR, "mailbox bench: wrong sums or a lost peer", nullptr);
+    *us = 1e3 * (double)ms / (double)iters;
+    return CFD_SUCCESS;
+}

@@ -154,8 +154,9 @@ typedef enum {
     HIP_KT_CG_SMALL = 14,  /* small grids: the whole CG solve in one cooperative launch */
     HIP_KT_RELAX2 = 15,    /* RB-SOR: one sweep of TWO iterations (k_rb2, one device, 3-D) */
     HIP_KT_CC_FUSED = 16,  /* cg_variant 1: the whole iteration in one z-march (k_ccf, one
-                              device, 3-D) */
-    HIP_KT_COUNT = 17
+                              device, 3-D); the first and the plain launches (version 3) */
+    HIP_KT_CC_FOLD = 17,   /* cg_variant 1: the k_ccf launches that also fold x (every 4th) */
+    HIP_KT_COUNT = 18
 } hip_kernel_timer_t;
 
 CFD_HIP_EXPORT hip_proj_config_t hip_proj_config_default(void);
@@ -227,17 +228,30 @@ CFD_HIP_EXPORT void hip_proj_reset_timing(hip_proj_ctx_t* ctx);
  * with the HIP_KT_COUNT of the header they were built against. */
 CFD_HIP_EXPORT int hip_proj_get_timing_n(hip_proj_ctx_t* ctx, double* total_ms,
                                          long long* launches, int capacity);
-/* Legacy getter without a capacity: writes the first HIP_KT_COUNT_V1 (15)
- * entries only, the count of the header it was first published with, so a
- * caller built against that header is never overrun. Use hip_proj_get_timing_n. */
-#define HIP_KT_COUNT_V1 15
+/* Legacy getter without a capacity: writes the first HIP_KT_COUNT_LEGACY (17)
+ * entries, the count of the last header that shipped it as the only getter
+ * (ABI version 1, round 4), so a caller built against that header gets every
+ * entry it sized its arrays for. Use hip_proj_get_timing_n. */
+#define HIP_KT_COUNT_LEGACY 17
 CFD_HIP_EXPORT void hip_proj_get_timing(hip_proj_ctx_t* ctx, double* total_ms, long long* launches);
+
+/* Effective shader clock of the single-reduction march (k_ccf) while timing is
+ * enabled: every workgroup of a sampled launch (two in eight: CG iterations
+ * 5 and 7 mod 8, a plain and an x-fold launch) stamps
+ * s_memtime (shader cycles) and s_memrealtime (the 100 MHz constant clock) at
+ * its start and end; *mhz = 100 * sum(d memtime) / sum(d memrealtime) over
+ * those workgroups, *workgroups = how many stamped. Reset by
+ * hip_proj_reset_timing. 0 and *mhz = 0 when nothing was sampled. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_get_clock_sample(hip_proj_ctx_t* ctx, double* mhz,
+                                                      long long* workgroups);
 
 /* ABI version of this header (bumped when a struct layout, an enum's count or
  * a signature changes) and of the loaded library: a caller checks
  * hip_proj_abi_version() == HIP_PROJ_ABI_VERSION. Version 2: HIP_KT_COUNT 17,
- * hip_proj_get_timing_n, projection_hip_cg1. */
-#define HIP_PROJ_ABI_VERSION 2
+ * hip_proj_get_timing_n, projection_hip_cg1. Version 3: HIP_KT_COUNT 18
+ * (HIP_KT_CC_FOLD split from HIP_KT_CC_FUSED), hip_proj_get_clock_sample,
+ * hip_proj_comm_mailbox_bench; the legacy getter writes 17 entries. */
+#define HIP_PROJ_ABI_VERSION 3
 CFD_HIP_EXPORT int hip_proj_abi_version(void);
 /* sha256 prefix (16 hex digits) of the sources the library was built from
  * (cfd_amd/_sha.py: csrc/hip, csrc/host, include/cfd_hip), embedded at
@@ -392,6 +406,17 @@ CFD_HIP_EXPORT int hip_proj_comm_size(const hip_proj_comm_t* comm);
  * (RCCL communicators; verified at creation, CFD_HIP_DEVICE_ALLREDUCE=0 turns it
  * off), 0 when they use ncclAllReduce / the in-process group. */
 CFD_HIP_EXPORT int hip_proj_comm_device_allreduce(const hip_proj_comm_t* comm);
+/* Collective microbenchmark of the CG dot all-reduce of an RCCL communicator
+ * (the N-rank per-iteration budget): `iters` two-value
+ * all-reduces of rank-dependent values, timed with events on a stream of its
+ * own. mode 0: all of them inside ONE one-wave kernel (the device mailbox's
+ * round trip, mbox_allreduce2); mode 1: one one-wave kernel launch per
+ * all-reduce (launch + mailbox, what a CG iteration pays); mode 2: one
+ * 2-value ncclAllReduce per iteration (the fallback). *us = microseconds per
+ * all-reduce; every rank checks the sums. CFD_ERROR_UNSUPPORTED for modes 0/1
+ * without a mailbox or for an in-process group. */
+CFD_HIP_EXPORT cfd_status_t hip_proj_comm_mailbox_bench(hip_proj_comm_t* comm, int iters,
+                                                        int mode, double* us);
 /* Slab context for rank comm_rank of the global nx*ny*nz grid (3-D only). The
  * communicator must outlive the context. */
 CFD_HIP_EXPORT hip_proj_ctx_t* hip_proj_create_slab(size_t nx, size_t ny, size_t nz,

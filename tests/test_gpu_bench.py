@@ -63,13 +63,29 @@ def test_bench_512_single_reduction_default(hip_lib):
     assert d["cg_iters_per_step"][0] > 0 and d["cg_iter_ms"] > 0
     cmp = d["cg_variant_compare"]
     assert cmp["cg_variant"] == 0 and cmp["cg_iters"] > 0
+    # the compare times the main run's first timed step (step 1 here): the
+    # same CG iteration count within the variants' rounding
+    assert cmp["step"] == 1 and abs(cmp["cg_iters"] - cmp["main_same_step"]["cg_iters"]) <= 2
+    # plain and fold launches apart, their counts summing to the iterations
+    sp = d["ccf_launches"]
+    assert sp["cc_fused"]["launches"] + sp["cc_fold"]["launches"] == sum(d["cg_iters_per_step"])
+    assert sp["cc_fold"]["avg_ms"] > sp["cc_fused"]["avg_ms"] > 0
+    # the march's effective shader clock over the timed region
+    clk = d["clock"]
+    assert clk["sampled_workgroups"] > 0 and 500.0 < clk["k_ccf_shader_MHz"] < 3000.0
+    # the reference caller's step on host buffers beside the resident one
+    pl = d["plugin_step"]
+    assert pl["full"]["cg_iters"] == pl["resident"]["cg_iters"] == pl["dirty_faces"]["cg_iters"]
+    assert pl["ms_full"] > pl["ms_resident"] > 0 and pl["ms_dirty_faces"] > 0
+    assert 0 < pl["pcie_share"]["full"] < 1
 
 
-@pytest.mark.parametrize("case,world,size", [("cavity", 2, 66), ("tg", 2, 66), ("cavity", 4, 66),
-                                             ("cavity", 8, 130)])
-def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
+@pytest.mark.parametrize("case,world,size,cgv", [("cavity", 2, 66, -1), ("tg", 2, 66, -1),
+                                                  ("cavity", 4, 66, 1), ("cavity", 8, 130, 1)])
+def test_bench_multi_rank_rehearsal(hip_lib, case, world, size, cgv):
     """N ranks over RCCL on the one device; 8 ranks is the driver's largest
-    launch (here 128 interior planes = 16 per rank)."""
+    launch (here 128 interior planes = 16 per rank). cgv -1: the bench's own
+    choice (textbook CG below 512^3), 1: the single-reduction slab form."""
     env = _env()
     env["CFD_BENCH_SHARED_GPU"] = "1"
     # c10d rendezvous on port 0: the agent binds a free port itself (a port
@@ -77,7 +93,8 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
            "bench.py", "--gpus", str(world),
-           "--size", str(size), "--steps", "2", "--warmup", "1", "--case", case]
+           "--size", str(size), "--steps", "2", "--warmup", "1", "--case", case,
+           "--cg-variant", str(cgv)]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     d = _last_json(r.stdout)
@@ -95,7 +112,7 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size):
     # the other CG variant measured beside the timed region
     # the other CG variant than the timed one (cavity slabs: single-reduction
     # timed, textbook beside it; Taylor-Green: the other way round)
-    assert d["cg_variant"] == (1 if case == "cavity" else 0)
+    assert d["cg_variant"] == (cgv if cgv >= 0 else 0)
     cmp = d["cg_variant_compare"]
     assert cmp["cg_variant"] == 1 - d["cg_variant"] and cmp["cg_iters"] > 0
     assert cmp["ms_per_cg_iter_wall"] > 0

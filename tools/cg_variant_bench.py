@@ -30,6 +30,10 @@ def main():
         shapes = [(512, 512, 257), (512, 512, 130), (512, 512, 66)]
     elif os.environ.get("SHAPES") == "slabs":  # rank 0's slab of 512^3 on 1, 2, 4, 8 ranks
         shapes = [(512, 512, 512), (512, 512, 257), (512, 512, 130), (512, 512, 66)]
+    elif os.environ.get("SHAPES") == "slab8":  # rank 0's slab of 512^3 on 8 ranks
+        shapes = [(512, 512, 66)]
+    elif os.environ.get("SHAPES") == "256":  # configs[1]'s grid on one device
+        shapes = [(256, 256, 256)]
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
     rng = np.random.default_rng(1)
     for nx, ny, nz in shapes:

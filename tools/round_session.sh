@@ -16,13 +16,13 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke exit $rc"; tail -2 gpurun_out/${TAG}_smoke.log; [ $rc -ne 0 ] && exit $rc
 [ "${PART:-all}" = "tests" ] && exit 0
 fi
-[ -n "$NO_PROF" ] || { TAG=$TAG ARGS="--size 512 --steps 1 --warmup 1 --no-cpu-baseline --no-compare-cg-variant" bash tools/gpu_profile.sh || exit $?; \
+[ -n "$NO_PROF" ] || { TAG=$TAG ARGS="--size 512 --steps 1 --warmup 1 --no-cpu-baseline --no-compare-cg-variant --no-plugin-step" bash tools/gpu_profile.sh || exit $?; \
   cp gpurun_out/prof_${TAG}/traffic.json profiles/${TAG}_traffic.json; }
 # the bench at the driver's settings under a rocprofv3 kernel trace (no CPU
 # baseline: its child processes stay out of the profiler), so the committed
 # kernel statistics and that line come from one run on one box
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_benchtrace -o run \
-    --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
+    --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-plugin-step \
     > gpurun_out/${TAG}_bench_traced.json 2> gpurun_out/${TAG}_bench_traced.err
 rc=$?; echo "traced bench exit $rc"; [ $rc -ne 0 ] && exit $rc
 f=$(find gpurun_out/${TAG}_benchtrace -name 'run_kernel_stats.csv' | head -n 1)
