@@ -116,6 +116,11 @@ def parse():
     return ap.parse_args()
 
 
+def progress(msg):
+    """A progress line on stderr (long runs: one every minute or so)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,8 +218,9 @@ def main():
             raise RuntimeError(f"step failed {s}: {_native.last_error()}")
         return ctx.poisson_stats().iterations
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         step()
+        progress(f"warm-up step {w + 1}/{args.warmup}")
     ctx.synchronize()
     ctx.reset_timing()
     ctx.enable_timing(True)
@@ -223,10 +229,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     iters, step_ms = [], []
-    for _ in range(args.steps):
+    for k in range(args.steps):
         ts = time.perf_counter()
         iters.append(step())  # returns after the step's CG solve has drained
         step_ms.append((time.perf_counter() - ts) * 1e3)
+        if k % 5 == 4:
+            progress(f"timed step {k + 1}/{args.steps}")
     ctx.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -342,6 +350,7 @@ def main():
     # the cos(pi x) cos(pi y) cos(pi z) RHS (interior mean removed), for the
     # CG variant of this context; the CG-iteration roofline without the
     # convergence tail or the step's other kernels
+    progress("timed region done")
     fixed200 = {}
     cos_rhs = None
     if world == 1 and not tg and args.fixed_cg_iters > 0:
@@ -363,6 +372,7 @@ def main():
     # the main run's own wall time of that step
     other = None
     if not args.no_compare_cg_variant:
+        progress("cg_variant_compare")
         ctx.close()
         ctx = make_ctx(1 - args.cg_variant)
         for _ in range(args.warmup):
@@ -406,12 +416,14 @@ def main():
     # step on the same steps; never `value`
     plug = None
     if world == 1 and not tg and not args.no_plugin_step:
+        progress("plugin_step")
         ctx.close()
         ctx = None
         plug = plugin_step(n, g, params, make_ctx, args.plugin_steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not tg:
+        progress("cpu_baseline")
         cpu = cpu_baseline(n, args, k_mean)
 
     if rank == 0:
@@ -475,6 +487,7 @@ def main():
                       "how": ("wave 0 of every workgroup of 2 in 8 k_ccf launches stamps "
                               "s_memtime / s_memrealtime at its start and end; MHz = 100 x "
                               "sum d memtime / sum d memrealtime (rank 0)")},
+            "box": box_id(torch, local),
             "step_ms": [round(v, 2) for v in step_ms],
             "cg_variant": args.cg_variant,
             "cg_variant_choice": cg_variant_choice(world, args),
@@ -859,6 +872,21 @@ def fixed_cg(ctx, g, params, n_int, cg_variant, cos_rhs, iters):
     return out
 
 
+def box_id(torch, device):
+    """Which box and card ran the line (host name, device name and UUID), so
+    lines from different boxes can be told apart when their rates differ."""
+    import socket
+    out = {"host": socket.gethostname()}
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        out["device"] = pr.name
+        uuid = getattr(pr, "uuid", None)
+        out["uuid"] = str(uuid) if uuid is not None else None
+    except Exception as e:  # noqa: BLE001
+        out["error"] = str(e)[:200]
+    return out
+
+
 def slab_budget():
     """The newest committed N-rank per-iteration budget
     (profiles/*_slab_budget.json, written by tools/slab_budget.py from
@@ -973,6 +1001,7 @@ def cpu_baseline(n, args, k_gpu):
     runs = {}
     for name, bind in (("bound", {"OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}),
                        ("unbound", {"OMP_PROC_BIND": "false"})):
+        progress(f"cpu_baseline placement {name}")
         env = dict(os.environ, OMP_NUM_THREADS=str(threads), CFD_AMD_NO_TORCH="1", **bind)
         if name == "unbound":
             env.pop("OMP_PLACES", None)

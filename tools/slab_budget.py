@@ -127,7 +127,8 @@ def allreduce_worker():
     dist.broadcast_object_list(uid, src=0)
     comm = api.SlabComm.rccl(uid[0], rank, world, 0)
     out = {"world": world, "device_allreduce": comm.device_allreduce}
-    iters = int(os.environ.get("CFD_BUDGET_AR_ITERS", "2000"))
+    # 8 processes sharing one GPU's queues time-slice: fewer exchanges there
+    iters = int(os.environ.get("CFD_BUDGET_AR_ITERS", "2000" if world <= 4 else "100"))
     for mode in (0, 1, 2):
         if mode < 2 and not comm.device_allreduce:
             continue
@@ -154,10 +155,19 @@ def allreduce_run(world):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0",
            "--local-addr=127.0.0.1", str(Path(__file__).resolve()), "--allreduce-worker"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
-    if r.returncode != 0:
-        return {"world": world, "error": (r.stdout + r.stderr)[-800:]}
-    for line in r.stdout.splitlines():
+    import signal
+    # its own process group: on a timeout the launcher AND its ranks go
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=150)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return {"world": world, "error": "timeout 150 s (ranks sharing one GPU's queues)"}
+    if p.returncode != 0:
+        return {"world": world, "error": (so + se)[-800:]}
+    for line in so.splitlines():
         if line.startswith("ALLREDUCE "):
             return json.loads(line[len("ALLREDUCE "):])
     return {"world": world, "error": "no result line"}
@@ -169,6 +179,9 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--worlds", default="2,4,8")
     ap.add_argument("--allreduce-worker", action="store_true")
+    ap.add_argument("--pieces", default="",
+                    help="reuse the pieces of an earlier run (its JSON) and measure only "
+                         "the all-reduce worlds they lack")
     args = ap.parse_args()
     if args.allreduce_worker:
         allreduce_worker()
@@ -177,6 +190,14 @@ def main():
 
     worlds = [int(w) for w in args.worlds.split(",") if w]
     t0 = time.time()
+    if args.pieces:
+        pieces = json.loads(Path(args.pieces).read_text())["pieces"]
+        ar = pieces.setdefault("allreduce", {})
+        for world in worlds:
+            if "mode0_us" not in ar.get(str(world), {}):
+                ar[str(world)] = allreduce_run(world)
+                print(json.dumps({"piece": "allreduce", **ar[str(world)]}), flush=True)
+        return finish(args, worlds, pieces, t0)
     pieces = {}
     one = {"cg1": per_iter(N, N, N, 1, args.iters), "cg0": per_iter(N, N, N, 0, args.iters)}
     pieces["one_gpu_512"] = {k: {"ms": v[0], "timers": v[1]} for k, v in one.items()}
@@ -202,7 +223,11 @@ def main():
         ar[str(world)] = allreduce_run(world)
         print(json.dumps({"piece": "allreduce", **ar[str(world)]}), flush=True)
     pieces["allreduce"] = ar
+    finish(args, worlds, pieces, t0)
 
+
+def finish(args, worlds, pieces, t0):
+    ar = pieces["allreduce"]
     halo_ms = (2.0 * N * N * 8 / (XGMI_GBPS * 1e9) * 1e3) + RCCL_US * 1e-3
     proj = {}
     t1 = pieces["one_gpu_512"]["cg1"]["ms"]
