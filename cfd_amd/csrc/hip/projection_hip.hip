@@ -1360,7 +1360,13 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             // 16 at 0.600-0.604 / 0.316-0.319 / 0.171 ms against 24's 0.613-
             // 0.615 / 0.317-0.318 / 0.169 and 32's 0.627-0.630 / 0.334-0.335 /
             // 0.197 (profiles/r05at_ccf_kc_thin_ab.jsonl)
-            cg.kc = (nint_k > 300) ? 24 : 16;
+            // r06: one device always 24 (256^3: 0.151-0.157 vs 16's 0.159-0.168
+            // ms per iteration in three same-box pairs, profiles/r06c_ccf_kc_256_ab.jsonl;
+            // the 16 of r05 was measured on 512^2 slab shapes only);
+            // Z-slabs: 16, and 11 on slabs of <= 100 planes (512^2 x 66, the
+            // 8-rank slab: 0.1615-0.1678 vs 16's 0.1706-0.1712, 13 0.1637-0.1693,
+            // 21 0.168, 32 0.189-0.197; profiles/r06c_ccf_kc_slab8_ab.jsonl)
+            cg.kc = (c->nranks == 1) ? 24 : (nint_k <= 100 ? 11 : 16);
             const char* ekc = getenv("CFD_HIP_CCF_KC");  // experiments
             if (ekc) cg.kc = std::max(1, atoi(ekc));
             const bool kc_fixed = getenv("CFD_HIP_CCF_KC_FIXED") != nullptr;

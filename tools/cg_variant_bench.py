@@ -32,6 +32,11 @@ def main():
         shapes = [(512, 512, 512), (512, 512, 257), (512, 512, 130), (512, 512, 66)]
     elif os.environ.get("SHAPES") == "slab8":  # rank 0's slab of 512^3 on 8 ranks
         shapes = [(512, 512, 66)]
+    elif os.environ.get("SHAPES") == "depth":  # 512^2 planes, 64 .. 510 interior planes
+        shapes = [(512, 512, 66), (512, 512, 130), (512, 512, 257), (512, 512, 386),
+                  (512, 512, 512)]
+    elif os.environ.get("SHAPES") == "slab4":  # rank 0's slab of 512^3 on 4 ranks
+        shapes = [(512, 512, 130)]
     elif os.environ.get("SHAPES") == "256":  # configs[1]'s grid on one device
         shapes = [(256, 256, 256)]
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
