@@ -208,7 +208,10 @@ def main():
     print(json.dumps({"piece": "one_gpu_512", **pieces["one_gpu_512"]}), flush=True)
     for world in worlds:
         P = slab_planes(world)
-        c1 = per_iter(N, N, P + 2, 1, args.iters)
+        # the slab interior launch's z-run length (projection_hip.hip init_ctx:
+        # 11 on slabs of <= 100 planes, else 16), forced on the one-device shape
+        kc = {"CFD_HIP_CCF_KC": "11" if P <= 100 else "16", "CFD_HIP_CCF_KC_FIXED": "1"}
+        c1 = per_iter(N, N, P + 2, 1, args.iters, kc)
         c0 = per_iter(N, N, P + 2, 0, args.iters)
         pieces[f"slab_{world}"] = {"planes": P, "march_P": {"ms": c1[0], "timers": c1[1]},
                                    "textbook_P": {"ms": c0[0], "timers": c0[1]}}
