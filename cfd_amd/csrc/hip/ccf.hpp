@@ -157,8 +157,13 @@ static __global__ __launch_bounds__(1024, 4) void k_ccf(
     } else {
         const int kt0 = (g.kmode == 2) ? g.kt0 : g.k0;
         const int kt1 = (g.kmode == 2) ? g.kt1 : g.k1;
-        kb = kt0 + tz * g.kc;
-        ke = min(kb + g.kc, kt1);
+        if (tz < g.nz1) {
+            kb = kt0 + tz * g.kc;
+            ke = min(kb + g.kc, kt1);
+        } else {  // tail layers: shorter runs (dispatched last)
+            kb = min(kt0 + g.nz1 * g.kc + (tz - g.nz1) * g.kc2, kt1);
+            ke = min(kb + g.kc2, kt1);
+        }
     }
     const bool jin = j >= 1 && j <= g.ny - 2;
     const bool in0 = jin && i0 >= 1 && i0 <= g.nx - 2;

@@ -143,6 +143,7 @@ struct hip_proj_ctx {
     // slabs, fused form: cc_int with stage c and a shared reduction, and
     // k_cc2's tiling of the two edge planes completing it (tiles_x 0: off)
     SGeo cc_int_red{}, cc2_edge{};
+    int ccf_tail = 0, ccf_kc2 = 0;       // k_ccf tail layers of shorter runs (ccf_layout)
     double* r2 = nullptr;                // k_ccf: r_{it+1} when r_it is in r (by parity)
     double* partials = nullptr;
     unsigned* counter = nullptr;

@@ -411,6 +411,11 @@ struct SGeo {
     // k_rb1: x of the first tile's first output column (the narrow
     // remainder strip starts where the full-width tiles end)
     int xofs;
+    // k_ccf (kmode 0 / 2): z layers tz < nz1 run kc planes from the range's
+    // start; layers tz >= nz1 ("tail") run kc2 planes from plane start +
+    // nz1 kc, so the last-dispatched workgroups are short (nz1 = tiles_z:
+    // every layer kc planes)
+    int kc2, nz1;
 };
 
 __device__ __forceinline__ int xcd_tile(int b, int nt) {

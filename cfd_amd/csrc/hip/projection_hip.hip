@@ -1181,6 +1181,28 @@ static void free_ctx(hip_proj_ctx* c) {
     delete c;
 }
 
+// k_ccf's z layers over P planes: runs of kc, and with tail_layers > 0 the
+// last tail_layers layers runs of kc2 (< kc) covering the remaining planes,
+// so the workgroups dispatched last are short and the launch's tail (each CU
+// idles while the last workgroups finish) shrinks. tail_layers = 0: every
+// layer kc.
+static void ccf_layout(SGeo& g, int P, int kc, int kc2, int tail_layers) {
+    kc = std::max(1, std::min(kc, P));
+    g.kc = kc;
+    g.kc2 = kc;
+    g.nz1 = g.tiles_z = (P + kc - 1) / kc;
+    if (tail_layers <= 0 || kc2 <= 0 || kc2 >= kc) return;
+    const int tail = std::min(P, tail_layers * kc2);
+    const int bulk = P - tail;
+    if (bulk <= 0) return;
+    g.kc2 = kc2;
+    g.nz1 = (bulk + kc - 1) / kc;
+    // the bulk's last layer may be partial: the tail then starts at nz1 kc,
+    // past the bulk, and covers P - nz1 kc planes
+    const int rest = std::max(0, P - g.nz1 * kc);
+    g.tiles_z = g.nz1 + (rest + kc2 - 1) / kc2;
+}
+
 static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1373,8 +1395,13 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
             while (!kc_fixed && cg.kc > 4 &&
                    (long long)cg.tiles_x * cg.tiles_y * ((nint_k + cg.kc - 1) / cg.kc) < 512)
                 cg.kc /= 2;
-            cg.kc = std::max(1, std::min(cg.kc, nint_k));
-            cg.tiles_z = (nint_k + cg.kc - 1) / cg.kc;
+            // tail layers of shorter runs (experiments: CFD_HIP_CCF_TAIL = layers,
+            // CFD_HIP_CCF_KC2 = their run length; default off)
+            const int tail_l = getenv("CFD_HIP_CCF_TAIL") ? atoi(getenv("CFD_HIP_CCF_TAIL")) : 0;
+            const int kc2 = getenv("CFD_HIP_CCF_KC2") ? atoi(getenv("CFD_HIP_CCF_KC2")) : cg.kc / 2;
+            c->ccf_tail = tail_l;
+            c->ccf_kc2 = kc2;
+            ccf_layout(cg, nint_k, cg.kc, kc2, tail_l);
             n_partials = std::max(n_partials, cg.tiles_x * cg.tiles_y * cg.tiles_z);
             // Z-slabs of >= 3 planes: the edge planes' launch (kmode 1) and
             // the interior planes' (kmode 2), so the r halo overlaps the latter
@@ -1390,8 +1417,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
                 m.kmode = 2;
                 m.kt0 = cg.k0 + 1;
                 m.kt1 = cg.k1 - 1;
-                m.kc = std::max(1, std::min(cg.kc, m.kt1 - m.kt0));
-                m.tiles_z = (m.kt1 - m.kt0 + m.kc - 1) / m.kc;
+                ccf_layout(m, m.kt1 - m.kt0, cg.kc, c->ccf_kc2, c->ccf_tail);
                 // fused form: the interior march with stage c (cc_int_red)
                 // and k_cc2 on the two edge planes (cc2_edge, the row-pair
                 // tiling of k_cc2 in kmode 1) share one reduction, the
