@@ -435,6 +435,9 @@ cfd_status_t ctx_shell_put(hip_proj_ctx* c, const double* const* host, double* c
                            int depth) __attribute__((visibility("hidden")));
 cfd_status_t ctx_shell_get(hip_proj_ctx* c, double* const* host, double* const* dev, int nf,
                            int depth) __attribute__((visibility("hidden")));
+// compute_max_temperature over a host array (the reference's sequential
+// result, computed on up to 16 threads; shell_io.hip).
+double ctx_host_max(const double* T, size_t n) __attribute__((visibility("hidden")));
 // Position-weighted 64-bit hashes of each host array's deep interior (all
 // indices in [2, n-3]; layer1 = false) or of the layer next to the boundary
 // (layer1 = true), multithreaded (shell_io.hip).

@@ -2313,12 +2313,9 @@ static cfd_status_t host_steps(hip_proj_ctx_t* c, flow_field* f, const grid* g,
         }
     }
     if (s == CFD_SUCCESS && stats && f->T && !shell) {
-        // compute_max_temperature (solver_registry.c:52-62) on the host copy
-        size_t n = c->nx * c->ny * c->nz;
-        double m = f->T[0];
-        for (size_t i = 1; i < n; i++)
-            if (f->T[i] > m) m = f->T[i];
-        stats->max_temperature = m;
+        // compute_max_temperature (solver_registry.c:52-62) on the host copy,
+        // threaded (r06: one core took ~0.1 s of a 512^3 host-buffer step)
+        stats->max_temperature = ctx_host_max(f->T, c->nx * c->ny * c->nz);
     }
     return s;
 }

@@ -145,7 +145,11 @@ void host_rows(const ShellMap& m, int nf, double* const* host, double* buf, bool
     th.reserve(nt);
     for (int t = 0; t < nt; ++t) {
         const long long r0 = nrows * t / nt, r1 = nrows * (t + 1) / nt;
-        th.emplace_back(work, r0, r1);
+        try {
+            th.emplace_back(work, r0, r1);
+        } catch (...) {  // no thread: this share on the caller's (C ABI)
+            work(r0, r1);
+        }
     }
     for (auto& t : th) t.join();
 }
@@ -207,6 +211,46 @@ cfd_status_t ctx_shell_get(hip_proj_ctx* c, double* const* host, double* const* 
     HIP_TRY(hipStreamSynchronize(c->stream));
     host_rows(m, nf, host, c->shell_host, false);
     return CFD_SUCCESS;
+}
+
+// compute_max_temperature (solver_registry.c:52-62) over a host array with
+// the reference's sequential semantics, m = T[0]; m = T[i] if T[i] > m, split
+// over up to 16 threads: each chunk's maximum from -inf with the same strict
+// comparison (its first occurrence; NaNs never compare greater), combined in
+// chunk order with that comparison, so the result is the sequential loop's
+// bit for bit (a NaN T[0] stays; -0.0 / +0.0 keep the earlier one).
+double ctx_host_max(const double* T, size_t n) {
+    if (n == 0) return 0.0;
+    unsigned hc = std::thread::hardware_concurrency();
+    int nt = (int)std::min<unsigned>(hc ? hc : 1, 16);
+    if (n < (1u << 20)) nt = 1;
+    std::vector<double> part(nt, -INFINITY);
+    auto work = [&](int t) {
+        const size_t a = 1 + (n - 1) * (size_t)t / (size_t)nt;
+        const size_t b = 1 + (n - 1) * (size_t)(t + 1) / (size_t)nt;
+        double m = -INFINITY;
+        for (size_t i = a; i < b; ++i)
+            if (T[i] > m) m = T[i];
+        part[t] = m;
+    };
+    if (nt == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(nt);
+        for (int t = 0; t < nt; ++t) {
+            try {
+                th.emplace_back(work, t);
+            } catch (...) {  // no thread: this share on the caller's (C ABI)
+                work(t);
+            }
+        }
+        for (auto& t : th) t.join();
+    }
+    double m = T[0];
+    for (double v : part)
+        if (v > m) m = v;
+    return m;
 }
 
 // Resident-mode guard (hip_proj_config_t.dirty_verify_interval): hashes of

@@ -190,3 +190,54 @@ def test_de_vahl_davis_ra1e3(hip_lib):
     assert abs(r["steps"] - want["steps"]) <= 2
     for k in ("umax", "vmax", "nu"):
         assert r[k] == pytest.approx(want[k], rel=1e-6), k
+
+
+def _seq_max(a):
+    """compute_max_temperature's loop (solver_registry.c:52-62): m = T[0];
+    m = T[i] if T[i] > m."""
+    m = a[0]
+    for v in a[1:]:
+        if v > m:
+            m = v
+    return m
+
+
+@pytest.mark.parametrize("plant", ["max_last_chunk", "nan_inside", "nan_first", "signed_zero"])
+def test_host_step_max_temperature_threaded(hip_lib, plant):
+    """The host-buffer step's stats.max_temperature (the full-transfer path
+    computes it on the caller's T, now on up to 16 threads, r06) equals the
+    reference's sequential loop bit for bit: a maximum in the last chunk, a
+    NaN inside (skipped by the strict comparison), a NaN at T[0] (kept), and
+    -0.0 / +0.0 ties (the first one kept). 130 x 130 x 66 = 1.1 M cells, so
+    the threaded path runs."""
+    g, f, p = cases.cavity(130, 130, 66, Re=100.0, dt=1e-4)
+    t = f.T.reshape(-1)
+    rng = np.random.default_rng(3)
+    t[...] = rng.uniform(290.0, 310.0, t.size)
+    if plant == "max_last_chunk":
+        t[-5] = 400.0
+    elif plant == "nan_inside":
+        t[t.size // 3] = np.nan
+        t[t.size // 2] = 350.0
+    elif plant == "nan_first":
+        t[0] = np.nan
+    else:
+        t[...] = -0.0
+        t[t.size // 2] = 0.0
+    want = _seq_max(t[: min(t.size, 8)]) if plant == "nan_first" else None
+    reg = api.Registry()
+    solver = reg.create("projection_hip")
+    try:
+        assert solver.init(g, p) == A.CFD_SUCCESS
+        st = A.SolverStats()
+        assert solver.step(f, g, p, st) == A.CFD_SUCCESS, api._native.last_error()
+    finally:
+        solver.close()
+    got = st.max_temperature
+    if plant == "nan_first":
+        assert np.isnan(got) and np.isnan(want)
+        return
+    ref = float(np.max(t[~np.isnan(t)])) if plant != "signed_zero" else -0.0
+    assert got == ref
+    if plant == "signed_zero":
+        assert np.signbit(got)  # -0.0 at T[0] stays: +0.0 > -0.0 is false
