@@ -178,6 +178,7 @@ struct hip_proj_ctx {
         bool rb1_alt = true;      // CFD_HIP_RB1_ALT=0: every k_rb1 sweep upwards
         bool rb1_fold = true;     // CFD_HIP_RB1_FOLD=0: separate k_rx_shell launch
         bool rk_pair = true;      // CFD_HIP_RK_PAIR=0: per-cell RK4 stage
+        bool alloc_contig = false;  // CFD_HIP_ALLOC=contig: contiguous field allocations
     } env;
     // timing
     int timing = 0;
@@ -198,7 +199,16 @@ struct hip_proj_ctx {
 static cfd_status_t dalloc(hip_proj_ctx* c, double** ptr, size_t n) {
     const size_t off = (size_t)c->allocs.size() * c->stagger_bytes;
     void* base = nullptr;
-    HIP_TRY(hipMalloc(&base, n * sizeof(double) + off));
+    // CFD_HIP_ALLOC=contig (experiments, r06): physically contiguous fields
+    // (hipDeviceMallocContiguous), so the march's plane-strided accesses
+    // translate through large pages whatever the box's memory history;
+    // falls back to hipMalloc when the driver cannot place one
+    if (c->env.alloc_contig &&
+        hipExtMallocWithFlags(&base, n * sizeof(double) + off, hipDeviceMallocContiguous) != hipSuccess) {
+        (void)hipGetLastError();
+        base = nullptr;
+    }
+    if (!base) HIP_TRY(hipMalloc(&base, n * sizeof(double) + off));
     c->allocs.push_back(base);
     *ptr = (double*)((char*)base + off);
     HIP_TRY(hipMemsetAsync(*ptr, 0, n * sizeof(double), c->stream));

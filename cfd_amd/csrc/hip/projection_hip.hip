@@ -1227,6 +1227,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         c->env.rb1_alt = ienv("CFD_HIP_RB1_ALT", 1) != 0;
         c->env.rb1_fold = ienv("CFD_HIP_RB1_FOLD", 1) != 0;
         c->env.rk_pair = ienv("CFD_HIP_RK_PAIR", 1) != 0;
+        c->env.alloc_contig = getenv("CFD_HIP_ALLOC") && strcmp(getenv("CFD_HIP_ALLOC"), "contig") == 0;
     }
     c->nx = nx;
     c->ny = ny;
