@@ -1209,6 +1209,15 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, c->device));
     c->grid_cap = std::max(64, prop.multiProcessorCount * 8);
+    // field k starts k x 4 KiB into its allocation (r06): the march reads
+    // r_it and p_{it-1} and writes p_it and r_{it+1} at equal offsets of
+    // different fields, and with every field 2 MiB-aligned those streams meet
+    // on the same HBM channels. 512^3 k_ccf, one box, four interleaved
+    // rounds: 1.026-1.055 ms per iteration against 1.039-1.089 unstaggered
+    // (2 / 1 / 8 KiB: 1.029-1.059 / 1.028-1.067 / 1.029-1.079,
+    // profiles/r06l_ccf_stagger_ab.jsonl; r06k another box, same order).
+    // CFD_HIP_FIELD_STAGGER=N overrides (0: aligned fields)
+    c->stagger_bytes = 4096;
     if (const char* e = getenv("CFD_HIP_FIELD_STAGGER")) c->stagger_bytes = (size_t)atol(e) / 256 * 256;
     {
         auto ienv = [](const char* name, int dflt) {
