@@ -149,3 +149,63 @@ def test_slab_cavity_steps(hip_lib):
     assert all(abs(h[0] - i) <= 1 for h, i in zip(hist[0], its1)), (hist[0], its1)
     for k in FIELDS:
         assert _rel(got[k], want[k]) <= 1e-10, k
+
+
+@pytest.mark.parametrize("tail,kc2", [("1", "12"), ("2", "5")])
+def test_ccf_tail_layout_vs_textbook_oracle(hip_lib, monkeypatch, tail, kc2):
+    """k_ccf's optional tail layers of shorter z runs (ccf_layout,
+    CFD_HIP_CCF_TAIL / _KC2, read at context creation; off by default, r06):
+    the march's z decomposition changes only the per-tile dot grouping, so
+    the solve stays within the single-reduction gates against the oracle's
+    textbook CG. 65^3 (63 planes: 24-plane bulk runs + the tail) and a
+    fixed-iteration run, bitwise equal iterates between two contexts of the
+    same layout."""
+    monkeypatch.setenv("CFD_HIP_CCF_TAIL", tail)
+    monkeypatch.setenv("CFD_HIP_CCF_KC2", kc2)
+    monkeypatch.setenv("CFD_HIP_CCF_KC", "24")
+    monkeypatch.setenv("CFD_HIP_CCF_KC_FIXED", "1")
+    n = 65
+    g, rhs = cases.cos_rhs(n, n)
+    xo = np.zeros_like(rhs)
+    so, sto = oracle.cg_solve(xo, rhs, g.dx, g.dy, g.dz)
+    ctx = api.HipProjection(n, n, n, **CC)
+    try:
+        x = np.zeros_like(rhs)
+        s, st = ctx.poisson_solve(A.HIP_POISSON_CG, x, rhs, g.dx, g.dy, g.dz)
+    finally:
+        ctx.close()
+    assert so == s == A.CFD_SUCCESS and st.status == A.POISSON_CONVERGED
+    assert abs(st.iterations - sto.iterations) <= 2, (st.iterations, sto.iterations)
+    assert abs(st.final_residual - sto.final_residual) <= 1e-8 * sto.initial_residual
+    d = (x - x.mean()) - (xo - xo.mean())
+    assert float(np.max(np.abs(d))) / float(np.max(np.abs(xo))) <= 1e-6
+
+
+def test_field_stagger_is_bitwise_neutral(hip_lib, monkeypatch):
+    """The default 4 KiB field stagger (r06) moves where fields sit in their
+    allocations, never what is computed: cavity steps with both CG forms
+    are bitwise equal to the unstaggered fields (CFD_HIP_FIELD_STAGGER=0)."""
+    n = 33
+    out = {}
+    for stagger in ("0", None):
+        if stagger is None:
+            monkeypatch.delenv("CFD_HIP_FIELD_STAGGER", raising=False)
+        else:
+            monkeypatch.setenv("CFD_HIP_FIELD_STAGGER", stagger)
+        for cgv in (0, 1):
+            g, f, p = cases.cavity(n, n, n, Re=400.0, dt=2e-3)
+            ctx = api.HipProjection(n, n, n, cg_variant=cgv)
+            try:
+                api.cavity_bc(f, 1.0)
+                ctx.upload(f)
+                for _ in range(3):
+                    assert ctx.step_device(g, p) == A.CFD_SUCCESS, api._native.last_error()
+                out[(stagger, cgv)] = {k: ctx.get_field(fid).copy() for k, fid in
+                                       (("u", A.HIP_FIELD_U), ("v", A.HIP_FIELD_V),
+                                        ("w", A.HIP_FIELD_W), ("p", A.HIP_FIELD_P))}
+            finally:
+                ctx.close()
+    for cgv in (0, 1):
+        for k in ("u", "v", "w", "p"):
+            a, b = out[("0", cgv)][k], out[(None, cgv)][k]
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (cgv, k)
