@@ -1216,8 +1216,12 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     // rounds: 1.026-1.055 ms per iteration against 1.039-1.089 unstaggered
     // (2 / 1 / 8 KiB: 1.029-1.059 / 1.028-1.067 / 1.029-1.079,
     // profiles/r06l_ccf_stagger_ab.jsonl; r06k another box, same order).
+    // Textbook CG's sweeps measured 0.8 % slower staggered (1.302-1.335 vs
+    // 1.292-1.302 ms, r06m, where the march gained 1.044-1.048 vs
+    // 1.038-1.062, profiles/r06m_stagger_both_cg_ab.jsonl), so the stagger
+    // is the single-reduction contexts' default only.
     // CFD_HIP_FIELD_STAGGER=N overrides (0: aligned fields)
-    c->stagger_bytes = 4096;
+    c->stagger_bytes = (c->cfg.cg_variant == 1) ? 4096 : 0;
     if (const char* e = getenv("CFD_HIP_FIELD_STAGGER")) c->stagger_bytes = (size_t)atol(e) / 256 * 256;
     {
         auto ienv = [](const char* name, int dflt) {
