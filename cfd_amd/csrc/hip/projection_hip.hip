@@ -1246,6 +1246,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     c->ny = ny;
     c->nz = nz;
     c->px = (long long)((nx + 7) / 8 * 8);
+    // CFD_HIP_ROW_PAD=N (experiments, r06): N more doubles per row (a
+    // multiple of 8), so that rows do not start on 4 KiB boundaries
+    if (const char* e = getenv("CFD_HIP_ROW_PAD")) c->px += (long long)(std::max(0, atoi(e)) / 8 * 8);
     c->ps = c->px * (long long)ny;
     Geo& g = c->geo;
     g.nx = (int)nx;
