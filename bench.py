@@ -208,6 +208,9 @@ def main():
         args.cg_variant = cg_variant_auto(n, world, args.case)
     solver_name = "projection_hip_cg1" if args.cg_variant == 1 else "projection_hip"
     ctx = make_ctx(args.cg_variant)
+    # placement draws of the CG fields at creation (hip_proj_get_placement):
+    # each draw's probe time per CG iteration and the one kept
+    place_ms, place_pick = ctx.placement()
 
     def step():
         if tg:  # periodic BCs on u, v, w, p before every step (collective on slabs)
@@ -488,6 +491,10 @@ def main():
                               "s_memtime / s_memrealtime at its start and end; MHz = 100 x "
                               "sum d memtime / sum d memrealtime (rank 0)")},
             "box": box_id(torch, local),
+            "placement": {"probe_ms_per_iter": place_ms, "picked": place_pick,
+                          "how": ("the CG fields allocated up to 4 times at context creation, "
+                                  "each set timed on a 12-iteration probe solve, the fastest "
+                                  "kept (projection_hip.hip placement_draws)")},
             "step_ms": [round(v, 2) for v in step_ms],
             "cg_variant": args.cg_variant,
             "cg_variant_choice": cg_variant_choice(world, args),

@@ -190,6 +190,7 @@ def _bind_hip(lib) -> None:
     _sig(lib, "hip_proj_get_timing", None, V, A.c_double_p, P(C.c_longlong))
     _sig(lib, "hip_proj_get_timing_n", C.c_int, V, A.c_double_p, P(C.c_longlong), C.c_int)
     _sig(lib, "hip_proj_get_clock_sample", C.c_int, V, P(C.c_double), P(C.c_longlong))
+    _sig(lib, "hip_proj_get_placement", C.c_int, V, P(C.c_double), C.c_int, P(C.c_int))
     _sig(lib, "hip_proj_abi_version", C.c_int)
     _sig(lib, "hip_proj_build_id", C.c_char_p)
     _sig(lib, "hip_proj_synchronize", C.c_int, V)

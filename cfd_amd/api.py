@@ -578,6 +578,14 @@ class HipProjection:
     def reset_timing(self):
         self._lib().hip_proj_reset_timing(self._ctx)
 
+    def placement(self):
+        """(per-draw probe ms per CG iteration, index kept) of the context's
+        placement draws (hip_proj_get_placement); ([], -1) without draws."""
+        buf = (C.c_double * 16)()
+        pick = C.c_int(-1)
+        n = self._lib().hip_proj_get_placement(self._ctx, buf, 16, C.byref(pick))
+        return [round(buf[i], 4) for i in range(min(n, 16))], pick.value
+
     def clock_sample(self):
         """(MHz, workgroups): the effective shader clock of the sampled k_ccf
         workgroups since reset_timing (hip_proj_get_clock_sample)."""

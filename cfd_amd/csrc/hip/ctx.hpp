@@ -144,6 +144,8 @@ struct hip_proj_ctx {
     // k_cc2's tiling of the two edge planes completing it (tiles_x 0: off)
     SGeo cc_int_red{}, cc2_edge{};
     int ccf_tail = 0, ccf_kc2 = 0;       // k_ccf tail layers of shorter runs (ccf_layout)
+    std::vector<float> placement_ms;     // placement draws: ms per probe iteration, per draw
+    int placement_pick = -1;             // the draw kept (-1: no draws)
     double* r2 = nullptr;                // k_ccf: r_{it+1} when r_it is in r (by parity)
     double* partials = nullptr;
     unsigned* counter = nullptr;

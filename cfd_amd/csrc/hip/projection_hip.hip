@@ -1617,6 +1617,126 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
     return CFD_SUCCESS;
 }
 
+// ---------------------------------------------------------------------------
+// Placement draws of the single-reduction CG's fields (r06). The march
+// (k_ccf) streams r_it and p_{it-1} in and p_it and r_{it+1} out at equal
+// offsets of different fields, and how fast it runs depends on where the
+// allocator placed those fields: in one process, six 512^3 contexts created
+// one after another ran 1.034-1.222 ms per iteration, each one stable to
+// 0.2 % (tools/alloc_lottery.py, profiles/r06s_alloc_lottery.jsonl; textbook
+// CG's sweeps spread 2.5 %). So a large single-reduction context draws its CG
+// fields (r, r2, the four p buffers, x) up to `draws` times, keeping every
+// draw allocated until the end so that each lands on other pages, times a
+// short fixed-iteration solve on each, keeps the fastest set and frees the
+// others. Speed only: the fields are zeroed afterwards and the arithmetic is
+// the same on any placement. CFD_HIP_PLACEMENT_DRAWS=N (default 4; 1: off).
+// ---------------------------------------------------------------------------
+static __global__ void k_probe_fill(double* f, long long n) {
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const unsigned h = (unsigned)(e * 2654435761ll) >> 12;
+        f[e] = (double)(h & 1023u) * (1.0 / 1024.0) - 0.5;
+    }
+}
+
+static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
+    constexpr int NF = 7;
+    double** slots[NF] = {&c->r, &c->r2, &c->pa, &c->pb, &c->pc4, &c->pd4, &c->pn};
+    const size_t n = field_elems(c);
+    const size_t fbytes = n * sizeof(double);
+    if (!c->r2) ST_TRY(dalloc(c, &c->r2, n));
+    // a short solve on a pseudo-random right-hand side (us, the predictor's
+    // output buffer, free at creation), no early exit; device time by events
+    hipEvent_t ea, eb;
+    HIP_TRY(hipEventCreate(&ea));
+    HIP_TRY(hipEventCreate(&eb));
+    hipExtLaunchKernelGGL(k_probe_fill, dim3(4096), dim3(256), 0, c->stream, nullptr, nullptr, 0,
+                          c->us, (long long)n);
+    const double h = 1.0 / (double)(c->nx - 1);
+    auto probe = [&](float* ms) -> cfd_status_t {
+        double* keep_rhs = c->rhs;
+        c->rhs = c->us;
+        HIP_TRY(hipMemsetAsync(c->pn, 0, fbytes, c->stream));
+        HIP_TRY(hipEventRecord(ea, c->stream));
+        const cfd_status_t s = cg_solve(c, h, h, h, DivCoef{}, RHS_FROM_ARRAY, 0.0, 0.0, 12, 1,
+                                        false);
+        c->rhs = keep_rhs;
+        HIP_TRY(hipEventRecord(eb, c->stream));
+        HIP_TRY(hipEventSynchronize(eb));
+        HIP_TRY(hipEventElapsedTime(ms, ea, eb));
+        return s == CFD_ERROR_MAX_ITER ? CFD_SUCCESS : s;
+    };
+    struct Draw {
+        double* f[NF];
+        void* base[NF];
+        float ms;
+    };
+    std::vector<Draw> got;
+    // the allocation a field lives in: dalloc placed it allocs[i] + i x stagger
+    auto base_of = [&](double* f) -> void* {
+        for (size_t i = 0; i < c->allocs.size(); ++i)
+            if ((char*)f - (char*)c->allocs[i] == (std::ptrdiff_t)(i * c->stagger_bytes))
+                return c->allocs[i];
+        return nullptr;
+    };
+    cfd_status_t st = CFD_SUCCESS;
+    for (int d = 0; d < draws && st == CFD_SUCCESS; ++d) {
+        Draw w{};
+        if (d > 0) {
+            size_t freeb = 0, total = 0;
+            if (hipMemGetInfo(&freeb, &total) != hipSuccess || freeb < (size_t)(1.25 * NF * fbytes))
+                break;
+            // a draw that cannot be allocated ends the draws (the context
+            // keeps the best so far; the partial draw's fields are freed
+            // with the context)
+            bool ok = true;
+            for (int q = 0; q < NF && ok; ++q) {
+                ok = dalloc(c, slots[q], n) == CFD_SUCCESS;
+                if (ok) w.base[q] = c->allocs.back();
+            }
+            if (!ok) {
+                (void)hipGetLastError();
+                break;
+            }
+        } else {
+            for (int q = 0; q < NF; ++q) w.base[q] = base_of(*slots[q]);
+        }
+        for (int q = 0; q < NF; ++q) w.f[q] = *slots[q];
+        st = probe(&w.ms);
+        got.push_back(w);
+    }
+    hipEventDestroy(ea);
+    hipEventDestroy(eb);
+    if (got.empty()) return st == CFD_SUCCESS ? CFD_ERROR : st;
+    size_t best = 0;
+    for (size_t d = 1; d < got.size(); ++d)
+        if (got[d].ms < got[best].ms) best = d;
+    for (int q = 0; q < NF; ++q) *slots[q] = got[best].f[q];
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (size_t d = 0; d < got.size(); ++d) {
+        if (d == best) continue;
+        for (int q = 0; q < NF; ++q) {
+            void* b = got[d].base[q];
+            auto it = std::find(c->allocs.begin(), c->allocs.end(), b);
+            if (b && it != c->allocs.end()) {
+                c->allocs.erase(it);
+                hipFree(b);
+                c->bytes -= std::min(c->bytes, fbytes);
+            }
+        }
+    }
+    c->placement_ms.clear();
+    for (auto& w : got) c->placement_ms.push_back(w.ms / 12.0f);
+    c->placement_pick = (int)best;
+    // a clean state: the probe's fields, its RHS buffer and the CG state
+    for (int q = 0; q < NF; ++q) HIP_TRY(hipMemsetAsync(*slots[q], 0, fbytes, c->stream));
+    HIP_TRY(hipMemsetAsync(c->us, 0, fbytes, c->stream));
+    HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
+    c->pstats = poisson_solver_stats_t{};
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return st;
+}
+
 static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t nz_global,
                                    SlabComm* comm, size_t kofs, const hip_proj_config_t* cfg) {
     if (!hip_projection_available()) {
@@ -1643,6 +1763,21 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
     if (init_ctx(c, nx, ny, nz_local) != CFD_SUCCESS) {
         free_ctx(c);
         return nullptr;
+    }
+    // placement draws of the single-reduction CG's fields (large one-device
+    // 3-D contexts; see placement_draws)
+    {
+        const char* e = getenv("CFD_HIP_PLACEMENT_DRAWS");
+        const int draws = e ? atoi(e) : 4;
+        const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
+        if (!comm && c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 25) &&
+            draws > 1 && c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
+            if (placement_draws(c, draws) != CFD_SUCCESS) {
+                set_err(CFD_ERROR, "projection_hip: placement draws of the CG fields failed");
+                free_ctx(c);
+                return nullptr;
+            }
+        }
     }
     if (comm && c->cfg.poisson_method != HIP_POISSON_CG) {
         // Z-slab ranks of a relaxation solver: what the first solve would set
@@ -1910,6 +2045,15 @@ void hip_proj_reset_timing(hip_proj_ctx_t* c) {
         hipMemsetAsync(c->clk, 0, 4 * sizeof(unsigned long long), c->stream);
         hipStreamSynchronize(c->stream);
     }
+}
+
+int hip_proj_get_placement(hip_proj_ctx_t* c, double* ms_per_iter, int capacity, int* picked) {
+    GroupHostLock hl_(c);
+    if (picked) *picked = c ? c->placement_pick : -1;
+    if (!c) return 0;
+    const int n = (int)c->placement_ms.size();
+    for (int i = 0; i < n && i < capacity && ms_per_iter; ++i) ms_per_iter[i] = c->placement_ms[i];
+    return n;
 }
 
 cfd_status_t hip_proj_get_clock_sample(hip_proj_ctx_t* c, double* mhz, long long* workgroups) {

@@ -244,13 +244,22 @@ CFD_HIP_EXPORT void hip_proj_get_timing(hip_proj_ctx_t* ctx, double* total_ms, l
  * hip_proj_reset_timing. 0 and *mhz = 0 when nothing was sampled. */
 CFD_HIP_EXPORT cfd_status_t hip_proj_get_clock_sample(hip_proj_ctx_t* ctx, double* mhz,
                                                       long long* workgroups);
+/* Placement draws of a large single-reduction context (one device, >= 2^25
+ * cells; CFD_HIP_PLACEMENT_DRAWS, default 4): at creation its CG fields are
+ * allocated up to that many times and the set whose short probe solve ran
+ * fastest is kept. Writes each draw's probe time (ms per CG iteration) into
+ * ms_per_iter[0 .. min(capacity, count) - 1] and the kept draw's index into
+ * *picked (-1: no draws); returns the number of draws. */
+CFD_HIP_EXPORT int hip_proj_get_placement(hip_proj_ctx_t* ctx, double* ms_per_iter, int capacity,
+                                          int* picked);
 
 /* ABI version of this header (bumped when a struct layout, an enum's count or
  * a signature changes) and of the loaded library: a caller checks
  * hip_proj_abi_version() == HIP_PROJ_ABI_VERSION. Version 2: HIP_KT_COUNT 17,
  * hip_proj_get_timing_n, projection_hip_cg1. Version 3: HIP_KT_COUNT 18
  * (HIP_KT_CC_FOLD split from HIP_KT_CC_FUSED), hip_proj_get_clock_sample,
- * hip_proj_comm_mailbox_bench; the legacy getter writes 17 entries. */
+ * hip_proj_get_placement, hip_proj_comm_mailbox_bench; the legacy getter
+ * writes 17 entries. */
 #define HIP_PROJ_ABI_VERSION 3
 CFD_HIP_EXPORT int hip_proj_abi_version(void);
 /* sha256 prefix (16 hex digits) of the sources the library was built from
