@@ -1629,7 +1629,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
 // draw allocated until the end so that each lands on other pages, times a
 // short fixed-iteration solve on each, keeps the fastest set and frees the
 // others. Speed only: the fields are zeroed afterwards and the arithmetic is
-// the same on any placement. CFD_HIP_PLACEMENT_DRAWS=N (default 4; 1: off).
+// the same on any placement. CFD_HIP_PLACEMENT_DRAWS=N (default 6; 1: off).
 // ---------------------------------------------------------------------------
 static __global__ void k_probe_fill(double* f, long long n) {
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -1641,6 +1641,7 @@ static __global__ void k_probe_fill(double* f, long long n) {
 
 static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
     constexpr int NF = 7;
+    constexpr int PROBE_IT = 16;  // probe solve: setup + 16 iterations (~20 ms at 512^3)
     double** slots[NF] = {&c->r, &c->r2, &c->pa, &c->pb, &c->pc4, &c->pd4, &c->pn};
     const size_t n = field_elems(c);
     const size_t fbytes = n * sizeof(double);
@@ -1658,7 +1659,7 @@ static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
         c->rhs = c->us;
         HIP_TRY(hipMemsetAsync(c->pn, 0, fbytes, c->stream));
         HIP_TRY(hipEventRecord(ea, c->stream));
-        const cfd_status_t s = cg_solve(c, h, h, h, DivCoef{}, RHS_FROM_ARRAY, 0.0, 0.0, 12, 1,
+        const cfd_status_t s = cg_solve(c, h, h, h, DivCoef{}, RHS_FROM_ARRAY, 0.0, 0.0, PROBE_IT, 1,
                                         false);
         c->rhs = keep_rhs;
         HIP_TRY(hipEventRecord(eb, c->stream));
@@ -1726,7 +1727,7 @@ static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
         }
     }
     c->placement_ms.clear();
-    for (auto& w : got) c->placement_ms.push_back(w.ms / 12.0f);
+    for (auto& w : got) c->placement_ms.push_back(w.ms / (float)PROBE_IT);
     c->placement_pick = (int)best;
     // a clean state: the probe's fields, its RHS buffer and the CG state
     for (int q = 0; q < NF; ++q) HIP_TRY(hipMemsetAsync(*slots[q], 0, fbytes, c->stream));
@@ -1768,7 +1769,7 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
     // 3-D contexts; see placement_draws)
     {
         const char* e = getenv("CFD_HIP_PLACEMENT_DRAWS");
-        const int draws = e ? atoi(e) : 4;
+        const int draws = e ? atoi(e) : 6;
         const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
         if (!comm && c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 25) &&
             draws > 1 && c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
