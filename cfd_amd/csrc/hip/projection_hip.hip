@@ -1629,7 +1629,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
 // draw allocated until the end so that each lands on other pages, times a
 // short fixed-iteration solve on each, keeps the fastest set and frees the
 // others. Speed only: the fields are zeroed afterwards and the arithmetic is
-// the same on any placement. CFD_HIP_PLACEMENT_DRAWS=N (default 6; 1: off).
+// the same on any placement. CFD_HIP_PLACEMENT_DRAWS=N (default 8; 1: off).
 // ---------------------------------------------------------------------------
 static __global__ void k_probe_fill(double* f, long long n) {
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -1769,7 +1769,7 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
     // 3-D contexts; see placement_draws)
     {
         const char* e = getenv("CFD_HIP_PLACEMENT_DRAWS");
-        const int draws = e ? atoi(e) : 6;
+        const int draws = e ? atoi(e) : 8;
         const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
         if (!comm && c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 25) &&
             draws > 1 && c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
