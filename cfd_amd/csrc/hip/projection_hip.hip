@@ -10,6 +10,8 @@
 // is no host round trip per iteration (the reference GPU path does two per
 // iteration, poisson_cg_gpu_solve.cuh:189-203).
 #include "ctx.hpp"
+
+#include <array>
 #include "rb2.hpp"
 #include "ccf.hpp"
 
@@ -1639,7 +1641,7 @@ static __global__ void k_probe_fill(double* f, long long n) {
     }
 }
 
-static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
+static cfd_status_t placement_draws(hip_proj_ctx* c, int sets, int trials) {
     constexpr int NF = 7;
     constexpr int PROBE_IT = 16;  // probe solve: setup + 16 iterations (~20 ms at 512^3)
     double** slots[NF] = {&c->r, &c->r2, &c->pa, &c->pb, &c->pc4, &c->pd4, &c->pn};
@@ -1667,12 +1669,10 @@ static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
         HIP_TRY(hipEventElapsedTime(ms, ea, eb));
         return s == CFD_ERROR_MAX_ITER ? CFD_SUCCESS : s;
     };
-    struct Draw {
-        double* f[NF];
-        void* base[NF];
-        float ms;
-    };
-    std::vector<Draw> got;
+    // the pool: the fields as created (set 0) and sets - 1 more allocations
+    // of all seven, every one kept until the end so each lands on other pages
+    std::vector<double*> pf;
+    std::vector<void*> pb;
     // the allocation a field lives in: dalloc placed it allocs[i] + i x stagger
     auto base_of = [&](double* f) -> void* {
         for (size_t i = 0; i < c->allocs.size(); ++i)
@@ -1680,54 +1680,80 @@ static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
                 return c->allocs[i];
         return nullptr;
     };
-    cfd_status_t st = CFD_SUCCESS;
-    for (int d = 0; d < draws && st == CFD_SUCCESS; ++d) {
-        Draw w{};
-        if (d > 0) {
-            size_t freeb = 0, total = 0;
-            if (hipMemGetInfo(&freeb, &total) != hipSuccess || freeb < (size_t)(1.25 * NF * fbytes))
-                break;
-            // a draw that cannot be allocated ends the draws (the context
-            // keeps the best so far; the partial draw's fields are freed
-            // with the context)
-            bool ok = true;
-            for (int q = 0; q < NF && ok; ++q) {
-                ok = dalloc(c, slots[q], n) == CFD_SUCCESS;
-                if (ok) w.base[q] = c->allocs.back();
+    for (int q = 0; q < NF; ++q) {
+        pf.push_back(*slots[q]);
+        pb.push_back(base_of(*slots[q]));
+    }
+    for (int d = 1; d < sets; ++d) {
+        size_t freeb = 0, total = 0;
+        if (hipMemGetInfo(&freeb, &total) != hipSuccess || freeb < (size_t)(1.25 * NF * fbytes))
+            break;
+        // a set that cannot be allocated ends the pool (its allocated part
+        // stays in it)
+        bool ok = true;
+        for (int q = 0; q < NF && ok; ++q) {
+            double* f = nullptr;
+            ok = dalloc(c, &f, n) == CFD_SUCCESS;
+            if (ok) {
+                pf.push_back(f);
+                pb.push_back(c->allocs.back());
             }
-            if (!ok) {
-                (void)hipGetLastError();
-                break;
-            }
-        } else {
-            for (int q = 0; q < NF; ++q) w.base[q] = base_of(*slots[q]);
         }
-        for (int q = 0; q < NF; ++q) w.f[q] = *slots[q];
-        st = probe(&w.ms);
-        got.push_back(w);
+        if (!ok) {
+            (void)hipGetLastError();
+            break;
+        }
+    }
+    // assignments of pool buffers to the seven roles: trial t < pool sets is
+    // set t as allocated; the rest draw seven distinct buffers (a fixed LCG)
+    const int npool = (int)pf.size();
+    const int nsets = npool / NF;
+    std::vector<std::array<int, NF>> asg;
+    unsigned long long lcg = 0x9E3779B97F4A7C15ull;
+    for (int t = 0; t < std::max(trials, 1); ++t) {
+        std::array<int, NF> a{};
+        if (t < nsets) {
+            for (int q = 0; q < NF; ++q) a[q] = t * NF + q;
+        } else {
+            std::vector<int> idx(npool);
+            for (int k = 0; k < npool; ++k) idx[k] = k;
+            for (int q = 0; q < NF; ++q) {
+                lcg = lcg * 6364136223846793005ull + 1442695040888963407ull;
+                const int k = q + (int)((lcg >> 33) % (unsigned long long)(npool - q));
+                std::swap(idx[q], idx[k]);
+                a[q] = idx[q];
+            }
+        }
+        asg.push_back(a);
+    }
+    cfd_status_t st = CFD_SUCCESS;
+    std::vector<float> ms(asg.size(), 0.f);
+    size_t done = 0;
+    for (; done < asg.size() && st == CFD_SUCCESS; ++done) {
+        for (int q = 0; q < NF; ++q) *slots[q] = pf[asg[done][q]];
+        st = probe(&ms[done]);
     }
     hipEventDestroy(ea);
     hipEventDestroy(eb);
-    if (got.empty()) return st == CFD_SUCCESS ? CFD_ERROR : st;
+    if (st != CFD_SUCCESS) return st;
     size_t best = 0;
-    for (size_t d = 1; d < got.size(); ++d)
-        if (got[d].ms < got[best].ms) best = d;
-    for (int q = 0; q < NF; ++q) *slots[q] = got[best].f[q];
+    for (size_t d = 1; d < done; ++d)
+        if (ms[d] < ms[best]) best = d;
+    for (int q = 0; q < NF; ++q) *slots[q] = pf[asg[best][q]];
     HIP_TRY(hipStreamSynchronize(c->stream));
-    for (size_t d = 0; d < got.size(); ++d) {
-        if (d == best) continue;
-        for (int q = 0; q < NF; ++q) {
-            void* b = got[d].base[q];
-            auto it = std::find(c->allocs.begin(), c->allocs.end(), b);
-            if (b && it != c->allocs.end()) {
-                c->allocs.erase(it);
-                hipFree(b);
-                c->bytes -= std::min(c->bytes, fbytes);
-            }
+    for (int k = 0; k < npool; ++k) {
+        bool used = false;
+        for (int q = 0; q < NF; ++q) used = used || asg[best][q] == k;
+        if (used) continue;
+        auto it = std::find(c->allocs.begin(), c->allocs.end(), pb[k]);
+        if (pb[k] && it != c->allocs.end()) {
+            c->allocs.erase(it);
+            hipFree(pb[k]);
+            c->bytes -= std::min(c->bytes, fbytes);
         }
     }
     c->placement_ms.clear();
-    for (auto& w : got) c->placement_ms.push_back(w.ms / (float)PROBE_IT);
+    for (size_t d = 0; d < done; ++d) c->placement_ms.push_back(ms[d] / (float)PROBE_IT);
     c->placement_pick = (int)best;
     // a clean state: the probe's fields, its RHS buffer and the CG state
     for (int q = 0; q < NF; ++q) HIP_TRY(hipMemsetAsync(*slots[q], 0, fbytes, c->stream));
@@ -1735,7 +1761,7 @@ static cfd_status_t placement_draws(hip_proj_ctx* c, int draws) {
     HIP_TRY(hipMemsetAsync(c->st, 0, sizeof(CgState), c->stream));
     c->pstats = poisson_solver_stats_t{};
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return st;
+    return CFD_SUCCESS;
 }
 
 static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t nz_global,
@@ -1770,10 +1796,15 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
     {
         const char* e = getenv("CFD_HIP_PLACEMENT_DRAWS");
         const int draws = e ? atoi(e) : 8;
+        // CFD_HIP_PLACEMENT_TRIALS (experiments): probes over the pool's
+        // buffers, the first `draws` the allocated sets, the rest random
+        // role assignments (default: the sets only)
+        const char* et = getenv("CFD_HIP_PLACEMENT_TRIALS");
+        const int trials = et ? std::max(1, atoi(et)) : draws;
         const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
         if (!comm && c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 25) &&
             draws > 1 && c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
-            if (placement_draws(c, draws) != CFD_SUCCESS) {
+            if (placement_draws(c, draws, trials) != CFD_SUCCESS) {
                 set_err(CFD_ERROR, "projection_hip: placement draws of the CG fields failed");
                 free_ctx(c);
                 return nullptr;
