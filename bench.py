@@ -492,9 +492,10 @@ def main():
                               "sum d memtime / sum d memrealtime (rank 0)")},
             "box": box_id(torch, local),
             "placement": {"probe_ms_per_iter": place_ms, "picked": place_pick,
-                          "how": ("the CG fields allocated up to 8 times at context creation, "
-                                  "each set timed on a 16-iteration probe solve, the fastest "
-                                  "kept (projection_hip.hip placement_draws)")},
+                          "how": ("the CG fields allocated 4 times at context creation, 24 "
+                                  "assignments of those buffers to the 7 roles each timed on "
+                                  "a 16-iteration probe solve, the fastest kept "
+                                  "(projection_hip.hip placement_draws)")},
             "step_ms": [round(v, 2) for v in step_ms],
             "cg_variant": args.cg_variant,
             "cg_variant_choice": cg_variant_choice(world, args),

@@ -581,10 +581,10 @@ class HipProjection:
     def placement(self):
         """(per-draw probe ms per CG iteration, index kept) of the context's
         placement draws (hip_proj_get_placement); ([], -1) without draws."""
-        buf = (C.c_double * 16)()
+        buf = (C.c_double * 64)()
         pick = C.c_int(-1)
-        n = self._lib().hip_proj_get_placement(self._ctx, buf, 16, C.byref(pick))
-        return [round(buf[i], 4) for i in range(min(n, 16))], pick.value
+        n = self._lib().hip_proj_get_placement(self._ctx, buf, 64, C.byref(pick))
+        return [round(buf[i], 4) for i in range(min(n, 64))], pick.value
 
     def clock_sample(self):
         """(MHz, workgroups): the effective shader clock of the sampled k_ccf

@@ -1631,7 +1631,9 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
 // draw allocated until the end so that each lands on other pages, times a
 // short fixed-iteration solve on each, keeps the fastest set and frees the
 // others. Speed only: the fields are zeroed afterwards and the arithmetic is
-// the same on any placement. CFD_HIP_PLACEMENT_DRAWS=N (default 8; 1: off).
+// the same on any placement. The probes also try random assignments of the
+// pool's buffers to the seven roles: what is slow is a PAIR of fields that
+// meet (r06x: random assignments from 4 sets beat 8 sets as allocated).
 // ---------------------------------------------------------------------------
 static __global__ void k_probe_fill(double* f, long long n) {
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -1794,13 +1796,17 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
     // placement draws of the single-reduction CG's fields (large one-device
     // 3-D contexts; see placement_draws)
     {
+        // a pool of 4 allocated sets and 24 probes: the 4 sets as allocated,
+        // then 20 random assignments of pool buffers to the seven roles.
+        // r06x, 512^3, contexts of one process (ms per iteration): none
+        // 1.109-1.201; 8 sets 1.037-1.126; 2 sets + 16 probes 1.033-1.047
+        // with one 1.198 (a pool with no good pair); 4 sets + 16 probes
+        // 1.030-1.044 (profiles/r06x_placement_strategies.jsonl).
+        // CFD_HIP_PLACEMENT_DRAWS = sets (1: off), _TRIALS = probes
         const char* e = getenv("CFD_HIP_PLACEMENT_DRAWS");
-        const int draws = e ? atoi(e) : 8;
-        // CFD_HIP_PLACEMENT_TRIALS (experiments): probes over the pool's
-        // buffers, the first `draws` the allocated sets, the rest random
-        // role assignments (default: the sets only)
+        const int draws = e ? atoi(e) : 4;
         const char* et = getenv("CFD_HIP_PLACEMENT_TRIALS");
-        const int trials = et ? std::max(1, atoi(et)) : draws;
+        const int trials = et ? std::max(1, atoi(et)) : 24;
         const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
         if (!comm && c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 25) &&
             draws > 1 && c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
