@@ -1793,8 +1793,8 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
         free_ctx(c);
         return nullptr;
     }
-    // placement draws of the single-reduction CG's fields (large one-device
-    // 3-D contexts; see placement_draws)
+    // placement draws of the single-reduction CG's fields (3-D contexts of
+    // >= 2^24 cells, one device or one Z-slab rank; see placement_draws)
     {
         // a pool of 4 allocated sets and 24 probes: the 4 sets as allocated,
         // then 20 random assignments of pool buffers to the seven roles.
@@ -1808,9 +1808,16 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
         const char* et = getenv("CFD_HIP_PLACEMENT_TRIALS");
         const int trials = et ? std::max(1, atoi(et)) : 24;
         const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
-        if (!comm && c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 25) &&
-            draws > 1 && c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
-            if (placement_draws(c, draws, trials) != CFD_SUCCESS) {
+        if (c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 24) && draws > 1 &&
+            c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {
+            // a Z-slab rank probes its own fields as one device (no halo,
+            // no all-reduce: nothing collective, so ranks may differ in how
+            // many sets their memory allows), the march over its local planes
+            const int nr = c->nranks;
+            c->nranks = 1;
+            const cfd_status_t ps = placement_draws(c, draws, trials);
+            c->nranks = nr;
+            if (ps != CFD_SUCCESS) {
                 set_err(CFD_ERROR, "projection_hip: placement draws of the CG fields failed");
                 free_ctx(c);
                 return nullptr;

@@ -244,8 +244,8 @@ CFD_HIP_EXPORT void hip_proj_get_timing(hip_proj_ctx_t* ctx, double* total_ms, l
  * hip_proj_reset_timing. 0 and *mhz = 0 when nothing was sampled. */
 CFD_HIP_EXPORT cfd_status_t hip_proj_get_clock_sample(hip_proj_ctx_t* ctx, double* mhz,
                                                       long long* workgroups);
-/* Placement draws of a large single-reduction context (one device, >= 2^25
- * cells): at creation its seven CG fields are allocated 4 times
+/* Placement draws of a large single-reduction context (3-D, >= 2^24 cells; a
+ * Z-slab rank probes its own fields as one device, nothing collective): at creation its seven CG fields are allocated 4 times
  * (CFD_HIP_PLACEMENT_DRAWS) and 24 assignments of those buffers to the seven
  * roles (CFD_HIP_PLACEMENT_TRIALS: the 4 sets, then random ones) are timed on a
  * short probe solve; the fastest is kept. Writes each draw's probe time (ms per CG iteration) into
