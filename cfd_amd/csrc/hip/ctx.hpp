@@ -181,6 +181,7 @@ struct hip_proj_ctx {
         bool rb1_fold = true;     // CFD_HIP_RB1_FOLD=0: separate k_rx_shell launch
         bool rk_pair = true;      // CFD_HIP_RK_PAIR=0: per-cell RK4 stage
         bool alloc_contig = false;  // CFD_HIP_ALLOC=contig: contiguous field allocations
+        bool ccf_edge_side = true;  // CFD_HIP_CCF_EDGE_SIDE=0: slab edge march before the interior
     } env;
     // timing
     int timing = 0;

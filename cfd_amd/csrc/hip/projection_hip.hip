@@ -182,23 +182,25 @@ static double* ccf_r1(hip_proj_ctx* c, int it) { return (it & 1) ? c->r : c->r2;
 
 template <bool FIRST, bool FOLD, bool NOC>
 static void launch_ccf_t(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
-                         const double* po, const PPrev& pv, double* x, int it, int xmap) {
+                         const double* po, const PPrev& pv, double* x, int it, int xmap,
+                         hipStream_t s) {
     // clock sample on one launch in eight while timing (iterations 5 and 7
     // mod 8: a plain and a fold launch)
     unsigned long long* clk = (c->timing && c->clk && (it & 5) == 5) ? c->clk : nullptr;
     hipExtLaunchKernelGGL((k_ccf<FIRST, FOLD, NOC>), dim3(g.tiles_x * g.tiles_y * g.tiles_z),
-                          dim3(1024), 0, c->stream, c->ta, c->tb, 0, g, L, ccf_r0(c, it),
+                          dim3(1024), 0, s, c->ta, c->tb, 0, g, L, ccf_r0(c, it),
                           ccf_r1(c, it), po, pn, pv, x, c->st, c->partials, c->counter, it, xmap,
                           dist(c) ? 1 : 0, c->dsum, mbox(c), clk);
 }
 
 template <bool NOC>
 static void launch_ccf_n(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
-                         const double* po, const PPrev& pv, double* x, int it, int xmap) {
+                         const double* po, const PPrev& pv, double* x, int it, int xmap,
+                         hipStream_t s) {
     const bool fold = (it % CG_XFOLD) == CG_XFOLD - 1;
-    if (it == 0) launch_ccf_t<true, false, NOC>(c, g, L, pn, po, pv, x, it, xmap);
-    else if (fold) launch_ccf_t<false, true, NOC>(c, g, L, pn, po, pv, x, it, xmap);
-    else launch_ccf_t<false, false, NOC>(c, g, L, pn, po, pv, x, it, xmap);
+    if (it == 0) launch_ccf_t<true, false, NOC>(c, g, L, pn, po, pv, x, it, xmap, s);
+    else if (fold) launch_ccf_t<false, true, NOC>(c, g, L, pn, po, pv, x, it, xmap, s);
+    else launch_ccf_t<false, false, NOC>(c, g, L, pn, po, pv, x, it, xmap, s);
 }
 
 // g: c->ccgeo (the whole march), or on Z-slabs c->cc_edge / c->cc_int. noc:
@@ -206,10 +208,12 @@ static void launch_ccf_n(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* p
 // planes), else it also forms w and the dot products (one device; a slab's
 // interior planes in the fused form)
 static void launch_ccf(hip_proj_ctx* c, const SGeo& g, const Lap& L, double* pn,
-                       const double* po, const PPrev& pv, double* x, int it, bool noc) {
+                       const double* po, const PPrev& pv, double* x, int it, bool noc,
+                       hipStream_t s = nullptr) {
     const int xmap = c->env.ccf_xmap;
-    if (noc) launch_ccf_n<true>(c, g, L, pn, po, pv, x, it, xmap);
-    else launch_ccf_n<false>(c, g, L, pn, po, pv, x, it, xmap);
+    if (!s) s = c->stream;
+    if (noc) launch_ccf_n<true>(c, g, L, pn, po, pv, x, it, xmap, s);
+    else launch_ccf_n<false>(c, g, L, pn, po, pv, x, it, xmap, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -358,9 +362,23 @@ static cfd_status_t cg_solve(hip_proj_ctx* c, double dx, double dy, double dz,
             double* r1 = ccf_r1(c, it);
             if (c->cc_edge.tiles_x > 0) {
                 const bool fused = c->cc2_edge.tiles_x > 0;
-                launch_ccf(c, c->cc_edge, L, pnew, pold, pv, x, it, true);
-                HIP_TRY(hipEventRecord(c->ev_b, c->stream));
-                HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
+                if (c->env.ccf_edge_side) {
+                    // r06: the edge planes' march runs on the side stream,
+                    // beside the interior march instead of before it: the
+                    // two read only r_it and p_{it-1} and write disjoint
+                    // planes of p_it, r_{it+1} and x (the interior march
+                    // forms the edge planes' r_{it+1} it needs itself), so
+                    // only the halo waits for the edge launch. The side
+                    // stream first waits for the main stream (the previous
+                    // iteration's reduction: alpha, beta)
+                    HIP_TRY(hipEventRecord(c->ev_b, c->stream));
+                    HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
+                    launch_ccf(c, c->cc_edge, L, pnew, pold, pv, x, it, true, c->hstream);
+                } else {
+                    launch_ccf(c, c->cc_edge, L, pnew, pold, pv, x, it, true);
+                    HIP_TRY(hipEventRecord(c->ev_b, c->stream));
+                    HIP_TRY(hipStreamWaitEvent(c->hstream, c->ev_b, 0));
+                }
                 double* rr[1] = {r1};
                 ST_TRY(timed_span(c, c->hstream, HIP_KT_HALO, [&] {
                     return c->comm->halo(c->hstream, rr, 1, c->ps, (int)c->nz, false);
@@ -1243,6 +1261,7 @@ static cfd_status_t init_ctx(hip_proj_ctx* c, size_t nx, size_t ny, size_t nz) {
         c->env.rb1_fold = ienv("CFD_HIP_RB1_FOLD", 1) != 0;
         c->env.rk_pair = ienv("CFD_HIP_RK_PAIR", 1) != 0;
         c->env.alloc_contig = getenv("CFD_HIP_ALLOC") && strcmp(getenv("CFD_HIP_ALLOC"), "contig") == 0;
+        c->env.ccf_edge_side = ienv("CFD_HIP_CCF_EDGE_SIDE", 1) != 0;
     }
     c->nx = nx;
     c->ny = ny;
