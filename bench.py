@@ -896,10 +896,18 @@ def box_id(torch, device):
 
 
 def slab_budget():
-    """The newest committed N-rank per-iteration budget
-    (profiles/*_slab_budget.json, written by tools/slab_budget.py from
-    one-GPU timings of each piece of a slab iteration), or None."""
-    for path in sorted((ROOT / "profiles").glob("*_slab_budget.json"), reverse=True):
+    """The committed N-rank per-iteration budget (written by
+    tools/slab_budget.py from one-GPU timings of each piece of a slab
+    iteration): the file profiles/slab_budget_current.json names, else the
+    newest profiles/*_slab_budget.json by name; None without one."""
+    cur = ROOT / "profiles" / "slab_budget_current.json"
+    paths = []
+    try:
+        paths.append(ROOT / "profiles" / json.loads(cur.read_text())["file"])
+    except (OSError, ValueError, KeyError, TypeError):
+        pass
+    paths += sorted((ROOT / "profiles").glob("*_slab_budget.json"), reverse=True)
+    for path in paths:
         try:
             d = json.loads(path.read_text())
         except (OSError, ValueError):
