@@ -22,11 +22,52 @@ from cfd_amd import api  # noqa: E402
 from tests import cases  # noqa: E402
 
 
+def relax_lottery(n, count, iters):
+    """METHOD=rbsor: the same for the RB-SOR solve (k_rb2 sweeps: X, rhs
+    in, the iterate out), per-iteration kernel time from the context's
+    relaxation timers."""
+    from cfd_amd import _abi as A
+    rhs = np.zeros((n, n, n))
+    rhs[1:-1, 1:-1, 1:-1] = np.cos(np.linspace(0, 3, n - 2))[None, None, :]
+    rhs -= rhs[1:-1, 1:-1, 1:-1].mean() * (rhs != 0)
+    d = 1.0 / (n - 1)
+    keep, res = [], []
+    for k in range(count):
+        c = api.HipProjection(n, n, n, poisson_method=A.HIP_POISSON_REDBLACK)
+        keep.append(c)
+        x = np.zeros((n, n, n))
+        c.poisson_solve(A.HIP_POISSON_REDBLACK, x, rhs, d, d, d,
+                        A.PoissonParams(0.0, 0.0, 3, 0.0, 1, False, 0))
+        t = []
+        for _ in range(2):
+            x[...] = 0.0
+            c.reset_timing()
+            c.enable_timing(True)
+            c.poisson_solve(A.HIP_POISSON_REDBLACK, x, rhs, d, d, d,
+                            A.PoissonParams(0.0, 0.0, iters, 0.0, 1, False, 0))
+            kt = c.timing()
+            c.enable_timing(False)
+            t.append((kt["relax"][0] + kt["relax2"][0] + kt["residual"][0]) / iters)
+        res.append(t)
+        print(json.dumps({"run": "alloc_lottery", "method": "rbsor", "context": k,
+                          "grid": [n, n, n], "ms_per_iter": [round(v, 4) for v in t]}), flush=True)
+    return keep, res
+
+
 def main():
     n = int(os.environ.get("N", "512"))
     count = int(os.environ.get("COUNT", "6"))
     iters = int(os.environ.get("ITERS", "60"))
     cgv = int(os.environ.get("CG_VARIANT", "1"))
+    if os.environ.get("METHOD") == "rbsor":
+        keep, res = relax_lottery(n, count, iters)
+        flat = [min(t) for t in res]
+        print(json.dumps({"run": "alloc_lottery_summary", "method": "rbsor",
+                          "min": round(min(flat), 4), "max": round(max(flat), 4),
+                          "spread": round(max(flat) / min(flat) - 1, 4)}), flush=True)
+        for c in keep:
+            c.close()
+        return
     g, rhs = cases.cos_rhs(n, n)
     rhs = np.ascontiguousarray(rhs)
     keep = []
