@@ -102,7 +102,14 @@ def parse():
                     help="0: textbook CG (the reference's loop); 1: single-reduction "
                          "(Chronopoulos-Gear) CG, one fused z-march per iteration; -1 "
                          "(default): 1 on one GPU at n >= 512, where it is measured faster "
-                         "(DESIGN.md section 5), else 0")
+                         "(DESIGN.md section 5); on N > 1 at 512^3 the committed budget's "
+                         "pick, then the live probe (--cg-probe); else 0")
+    ap.add_argument("--cg-probe", choices=("auto", "on", "off"), default="auto",
+                    help="N > 1: step both CG forms from fresh contexts before the run and "
+                         "keep the faster per CG iteration (auto: when --cg-variant is -1 "
+                         "on the 512^3 cavity)")
+    ap.add_argument("--cg-probe-steps", type=int, default=2,
+                    help="timed steps per form in the probe (after one untimed step)")
     ap.add_argument("--fixed-cg-iters", type=int, default=200,
                     help="fixed-iteration CG microbench per variant after the timed region "
                          "(SURVEY.md §8d config 3; 0: skip)")
@@ -204,13 +211,7 @@ def main():
         c.synchronize()
         return c
 
-    if args.cg_variant < 0:
-        args.cg_variant = cg_variant_auto(n, world, args.case)
-    solver_name = "projection_hip_cg1" if args.cg_variant == 1 else "projection_hip"
-    ctx = make_ctx(args.cg_variant)
-    # placement draws of the CG fields at creation (hip_proj_get_placement):
-    # each draw's probe time per CG iteration and the one kept
-    place_ms, place_pick = ctx.placement()
+    ctx = None
 
     def step():
         if tg:  # periodic BCs on u, v, w, p before every step (collective on slabs)
@@ -220,6 +221,51 @@ def main():
         if s != A.CFD_SUCCESS:
             raise RuntimeError(f"step failed {s}: {_native.last_error()}")
         return ctx.poisson_stats().iterations
+
+    def timed_steps(nsteps):
+        """(max-over-ranks seconds, CG iterations) of the next nsteps steps."""
+        ctx.synchronize()
+        if world > 1:
+            dist.barrier()
+        ta = time.perf_counter()
+        its = sum(step() for _ in range(nsteps))
+        ctx.synchronize()
+        e = time.perf_counter() - ta
+        if world > 1:
+            tt = torch.tensor([e], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            e = float(tt[0])
+        return e, its
+
+    auto = args.cg_variant < 0
+    if auto:
+        args.cg_variant = cg_variant_auto(n, world, args.case)
+    probe = None
+    if cg_probe_wanted(args, n, world, auto):
+        # N > 1: both CG forms step the trajectory's first steps on THIS node
+        # (fresh contexts, the first step untimed), the faster per CG
+        # iteration is the run's; every rank takes the same max-over-ranks
+        # times, so every rank picks the same form
+        progress("cg_variant probe")
+        probe = {"steps": f"{1 + args.cg_probe_steps} per form from a fresh context, "
+                          f"the first untimed (max over ranks)"}
+        for v in (args.cg_variant, 1 - args.cg_variant):
+            ctx = make_ctx(v)
+            step()
+            e, its = timed_steps(args.cg_probe_steps)
+            ctx.close()
+            ctx = None
+            probe[f"cg{v}"] = {"cg_iters": its, "ms": round(e * 1e3, 3),
+                               "ms_per_cg_iter": round(e * 1e3 / max(1, its), 5)}
+        faster = 1 if probe["cg1"]["ms_per_cg_iter"] < probe["cg0"]["ms_per_cg_iter"] else 0
+        probe["budget_pick"] = args.cg_variant
+        probe["picked"] = faster
+        args.cg_variant = faster
+    solver_name = "projection_hip_cg1" if args.cg_variant == 1 else "projection_hip"
+    ctx = make_ctx(args.cg_variant)
+    # placement draws of the CG fields at creation (hip_proj_get_placement):
+    # each draw's probe time per CG iteration and the one kept
+    place_ms, place_pick = ctx.placement()
 
     for w in range(args.warmup):
         step()
@@ -498,7 +544,7 @@ def main():
                                   "(projection_hip.hip placement_draws)")},
             "step_ms": [round(v, 2) for v in step_ms],
             "cg_variant": args.cg_variant,
-            "cg_variant_choice": cg_variant_choice(world, args),
+            "cg_variant_choice": cg_variant_choice(world, args, probe),
             "cg_variant_compare": other,
             "plugin_step": plug,
             "cg_fixed200": ({"iterations": args.fixed_cg_iters, "x0": "zero",
@@ -941,7 +987,17 @@ def cg_variant_auto(n, world, case="cavity"):
     return 1 if proj["cg1"] < proj["cg0"] else 0
 
 
-def cg_variant_choice(world, args):
+def cg_probe_wanted(args, n, world, auto):
+    """The live probe of both CG forms (N > 1): by default where the variant
+    is the bench's own choice on the cavity at the metric's 512^3 (the
+    committed budget is a one-GPU projection; the node running the line
+    settles it); --cg-probe on / off forces it either way."""
+    if args.cg_probe == "off" or args.case != "cavity" or world == 1:
+        return False
+    return args.cg_probe == "on" or (auto and n == 512)
+
+
+def cg_variant_choice(world, args, probe=None):
     """Why this run's CG variant was chosen (the bench line's record)."""
     if args.case != "cavity":
         return {"rule": "Taylor-Green: textbook CG"}
@@ -949,10 +1005,15 @@ def cg_variant_choice(world, args):
         return {"rule": "one GPU at n >= 512: single-reduction march (k_ccf)"}
     b = slab_budget()
     proj = (b or {}).get("projected_ms_per_iter", {}).get(str(world))
-    return {"rule": "N > 1: the lower projected per-iteration time of the committed slab "
-                    "budget at this N (textbook CG without one)",
-            "budget_file": b["file"] if b else None, "projected_ms_per_iter": proj,
-            "measured_on": (b or {}).get("measured_on")}
+    out = {"rule": "N > 1: the lower projected per-iteration time of the committed slab "
+                   "budget at this N (textbook CG without one)",
+           "budget_file": b["file"] if b else None, "projected_ms_per_iter": proj,
+           "measured_on": (b or {}).get("measured_on")}
+    if probe is not None:
+        out["rule"] = ("N > 1: the form with the lower wall time per CG iteration in the live "
+                       "probe on this node (the committed budget's pick beside it)")
+        out["probe"] = probe
+    return out
 
 
 def prof_record(prof, kname, key=None):

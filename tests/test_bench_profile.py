@@ -85,3 +85,19 @@ def test_sweep_symbols_track_the_variant():
                    "cc_spmv": "k_cc2<16, true, false, false>"}
     # the edge planes' k_cc2: 8 B per edge-plane cell, per slab cell 8 x 2 / planes
     assert dict((t, b) for t, _, b in bench.sweep_kernels(16, True, 15, 1, 64))["cc_spmv"] == 0.25
+
+
+def test_cg_probe_rule():
+    import argparse
+    a = lambda probe, case="cavity": argparse.Namespace(cg_probe=probe, case=case)
+    # default: N > 1, the bench's own choice, at the metric's 512^3 only
+    assert bench.cg_probe_wanted(a("auto"), 512, 8, True)
+    assert not bench.cg_probe_wanted(a("auto"), 512, 8, False)  # --cg-variant given
+    assert not bench.cg_probe_wanted(a("auto"), 256, 8, True)
+    assert not bench.cg_probe_wanted(a("auto"), 512, 1, True)   # one GPU: settled
+    assert not bench.cg_probe_wanted(a("auto", "tg"), 512, 8, True)
+    assert bench.cg_probe_wanted(a("on"), 66, 2, False)
+    assert not bench.cg_probe_wanted(a("on"), 66, 1, True)
+    assert not bench.cg_probe_wanted(a("off"), 512, 8, True)
+    ch = bench.cg_variant_choice(2, a("auto"), {"picked": 1})
+    assert ch["probe"] == {"picked": 1} and "live probe" in ch["rule"]

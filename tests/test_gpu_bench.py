@@ -80,12 +80,17 @@ def test_bench_512_single_reduction_default(hip_lib):
     assert 0 < pl["pcie_share"]["full"] < 1
 
 
-@pytest.mark.parametrize("case,world,size,cgv", [("cavity", 2, 66, -1), ("tg", 2, 66, -1),
-                                                  ("cavity", 4, 66, 1), ("cavity", 8, 130, 1)])
-def test_bench_multi_rank_rehearsal(hip_lib, case, world, size, cgv):
+@pytest.mark.parametrize("case,world,size,cgv,probe", [("cavity", 2, 66, -1, "auto"),
+                                                        ("tg", 2, 66, -1, "auto"),
+                                                        ("cavity", 2, 66, -1, "on"),
+                                                        ("cavity", 4, 66, 1, "auto"),
+                                                        ("cavity", 8, 130, 1, "auto")])
+def test_bench_multi_rank_rehearsal(hip_lib, case, world, size, cgv, probe):
     """N ranks over RCCL on the one device; 8 ranks is the driver's largest
     launch (here 128 interior planes = 16 per rank). cgv -1: the bench's own
-    choice (textbook CG below 512^3), 1: the single-reduction slab form."""
+    choice (textbook CG below 512^3), 1: the single-reduction slab form;
+    probe "on": both forms step first and the faster per CG iteration runs
+    (the default at 512^3 on N > 1)."""
     env = _env()
     env["CFD_BENCH_SHARED_GPU"] = "1"
     # c10d rendezvous on port 0: the agent binds a free port itself (a port
@@ -94,7 +99,7 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size, cgv):
            "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
            "bench.py", "--gpus", str(world),
            "--size", str(size), "--steps", "2", "--warmup", "1", "--case", case,
-           "--cg-variant", str(cgv)]
+           "--cg-variant", str(cgv), "--cg-probe", probe]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     d = _last_json(r.stdout)
@@ -112,7 +117,17 @@ def test_bench_multi_rank_rehearsal(hip_lib, case, world, size, cgv):
     # the other CG variant measured beside the timed region
     # the other CG variant than the timed one (cavity slabs: single-reduction
     # timed, textbook beside it; Taylor-Green: the other way round)
-    assert d["cg_variant"] == (cgv if cgv >= 0 else 0)
+    choice = d["cg_variant_choice"]
+    if probe == "on":
+        pr = choice["probe"]
+        assert pr["budget_pick"] == 0 and d["cg_variant"] == pr["picked"]
+        # both forms stepped the same steps of the trajectory
+        assert pr["cg0"]["cg_iters"] > 0 and pr["cg1"]["cg_iters"] > 0
+        faster = min((0, 1), key=lambda v: pr[f"cg{v}"]["ms_per_cg_iter"])
+        assert pr["picked"] == faster
+    else:
+        assert "probe" not in choice
+        assert d["cg_variant"] == (cgv if cgv >= 0 else 0)
     cmp = d["cg_variant_compare"]
     assert cmp["cg_variant"] == 1 - d["cg_variant"] and cmp["cg_iters"] > 0
     assert cmp["ms_per_cg_iter_wall"] > 0
