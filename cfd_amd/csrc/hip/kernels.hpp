@@ -2084,6 +2084,7 @@ struct RxState {
     // host-resolved exact residual of iterate ovr_it (-1: none), and max |rhs|
     int res_it, res_exact, ovr_it, pad0;
     double ovr_m, bmax;
+    double xmax;  // max |X| of a k_rb2 sweep's input when it certifies X (k_rb2_xmax)
 };
 
 constexpr int RX_RED = 0;

@@ -622,6 +622,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     cf.escale = 1.0;
     cf.mlim = 0x1p800;
     cf.slow = 0x1p-900;
+    cf.nif = -rc.inv_factor;
     if (c->env.rb2_test) {  // tests: force the host paths
         const int v = c->env.rb2_test;
         if (v == 1) cf.escale = 1e300;  // every approximate decision ambiguous
@@ -661,6 +662,15 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         } else {
             const int certx = (force_certx || log.empty() || log.back().kind == 1) ? 1 : 0;
             force_certx = false;
+            if (apx && certx) {  // X's own values: max |X| for the sweep's range test
+                // (an error here is sticky: the loop's next HIP_TRY reports it)
+                (void)hipMemsetAsync(&c->rxst->xmax, 0, sizeof(double), c->stream);
+                const int nbm = (int)std::min<long long>(
+                    4LL * c->grid_cap, ((long long)c->nx * c->ny * c->nz + 255) / 256);
+                hipExtLaunchKernelGGL(k_rb2_xmax, dim3(std::max(1, nbm)), dim3(256), 0,
+                                      c->stream, c->ta, c->tb, 0, c->geo, (const double*)bx,
+                                      c->rxst);
+            }
             timed(c, HIP_KT_RELAX2, [&] {
                 if (apx)
                     hipExtLaunchKernelGGL((k_rb2<true, FLR>), dim3(nb2), dim3(1024), 0, c->stream,
@@ -699,6 +709,7 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
         return -1;
     };
     const ResCoef resc{rc.dx2, rc.dy2, rc.inv_dz2};
+    static_assert(sizeof(RxState) <= sizeof(CgState), "h_state holds RxState copies");
     RxState* hs = reinterpret_cast<RxState*>(c->h_state);
     for (;;) {
         int chunk = 8, slot = 0, prev = -1;
@@ -943,6 +954,7 @@ static cfd_status_t relax_solve_fused(hip_proj_ctx* c, int method, const RelaxCo
     };
     // iterations 0..max_iter: sweep it also yields the residual after it - 1
     // iterations, so the last launch only completes the final test
+    static_assert(sizeof(RxState) <= sizeof(CgState), "h_state holds RxState copies");
     RxState* hs = reinterpret_cast<RxState*>(c->h_state);  // pinned, >= 3 RxState
     int it = 0, chunk = 8, slot = 0, prev = -1;
     const int chunk_max = std::max(1, c->cfg.poll_interval);

@@ -86,6 +86,7 @@ struct Rb2Coef {
     // sum| of one of its lanes is below it (2^-900; 1e300: every update)
     double escale, mlim;
     double slow;
+    double nif;  // -inv_factor: pn = t * nif is RN(-t * inv_factor) bit for bit (RN is odd)
 };
 
 // LDS of one k_rb2 workgroup (148 KB): X by plane parity, and the one-colour
@@ -119,28 +120,31 @@ __device__ __forceinline__ double rb2_div(double a, double d, double r) {
 
 // One SOR update from the neighbour sums sx = right + left, sy = up + down,
 // sz = above + below (linear_solver_redblack.c:103-112 order, as sor1)
+// (pn = -t / factor as t times the negated reciprocal: the same rounding, one
+// instruction fewer than a negation and a product)
 template <bool APX>
-__device__ __forceinline__ double rb2_sor(const RelaxCoef& rc, double vc, double sx, double sy,
-                                          double sz, double vb, double* tout = nullptr) {
+__device__ __forceinline__ double rb2_sor(const RelaxCoef& rc, double nif, double vc, double sx,
+                                          double sy, double sz, double vb,
+                                          double* tout = nullptr) {
     const double t = vb - rb2_div<APX>(sx, rc.dx2, rc.rdx2) - rb2_div<APX>(sy, rc.dy2, rc.rdy2) -
                      sz * rc.inv_dz2;
     if (tout) *tout = t;
-    const double pn = -t * rc.inv_factor;
+    const double pn = t * nif;
     return vc + rc.omega * (pn - vc);
 }
 
 // the approximate residual of the cell an update just touched, from the
 // update's own t = b - sx/dx^2 - sy/dy^2 - sz/dz^2 (lap - b = -t - k2 c):
-// one FMA, within the same bound as rb2_res_apx
+// one FMA, within the same bound as rb2_res_apx. Signed (its negation, as
+// fma rounds oddly): the running maximum takes |.| in its own instruction
 __device__ __forceinline__ double rb2_res_from_t(const Rb2Coef& cf, double c, double t) {
-    return fabs(fma(c, -cf.k2, -t));
+    return fma(c, cf.k2, t);
 }
 
-// approximate |lap(x) - rhs| from the neighbour sums (see the header)
+// approximate lap(x) - rhs from the neighbour sums (see the header), signed
 __device__ __forceinline__ double rb2_res_apx(const Rb2Coef& cf, double c, double sx, double sy,
                                               double sz, double b) {
-    return fabs(fma(sx, cf.rc.rdx2, fma(sy, cf.rc.rdy2, fma(sz, cf.rc.inv_dz2,
-                                                            fma(c, -cf.k2, -b)))));
+    return fma(sx, cf.rc.rdx2, fma(sy, cf.rc.rdy2, fma(sz, cf.rc.inv_dz2, fma(c, -cf.k2, -b))));
 }
 
 // the binary exponent of v as frexp gives it (0 for zero)
@@ -183,15 +187,14 @@ __device__ __forceinline__ double rb2_min_abs2(double a, double b) {
 // them, and costs two more per update). Either way the value is the
 // reference's.
 template <bool APX>
-__device__ __forceinline__ double rb2_sorc(const RelaxCoef& rc, double slow, double vc,
-                                           double sx, double sy, double sz, double vb,
-                                           double* tout = nullptr) {
+__device__ __forceinline__ double rb2_sorc(const Rb2Coef& cf, double vc, double sx, double sy,
+                                           double sz, double vb, double* tout = nullptr) {
     if constexpr (!APX) {
-        return rb2_sor<false>(rc, vc, sx, sy, sz, vb, tout);
+        return rb2_sor<false>(cf.rc, cf.nif, vc, sx, sy, sz, vb, tout);
     } else {
-        double v = rb2_sor<true>(rc, vc, sx, sy, sz, vb, tout);
-        if (__builtin_amdgcn_ballot_w64(rb2_min_abs2(sx, sy) < slow) != 0)
-            v = rb2_sor<false>(rc, vc, sx, sy, sz, vb, tout);
+        double v = rb2_sor<true>(cf.rc, cf.nif, vc, sx, sy, sz, vb, tout);
+        if (__builtin_amdgcn_ballot_w64(rb2_min_abs2(sx, sy) < cf.slow) != 0)
+            v = rb2_sor<false>(cf.rc, cf.nif, vc, sx, sy, sz, vb, tout);
         return v;
     }
 }
@@ -233,14 +236,15 @@ __device__ __forceinline__ bool rb2_decide(RxState* st, double m, double E, int 
 }
 
 // X = iterate s (s >= 1, its boundary shell Neumann), Y <- iterate s + 2.
-// certx: certify X's values too (the first sweep after a k_rb1 sweep).
+// X's own values are certified by k_rb2_xmax before the sweeps that need it
+// (certx: the first sweep after a k_rb1 sweep), not in the march.
 // The march of one k_rb2 tile (see the header); BND: the tile touches the
 // faces (per-lane face, range and shell logic), else all of it folds away.
 template <bool APX, int FL, bool BND>
 __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coef& cf,
                                           const double* __restrict__ X, double* __restrict__ Y,
                                           const double* __restrict__ rhs, int c, int r, int i0,
-                                          int j, int kb, int ke, int certx, double& mX,
+                                          int j, int kb, int ke, double& mX,
                                           double& mY, double& M) {
     const RelaxCoef& rc = cf.rc;
     // LDS addressing: two per-lane bases (planes 0-7 and 8-15), each at the
@@ -342,7 +346,6 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         if constexpr (APX) asm volatile("" : "+v"(M));
     };
     const int nzi = g.nz - 2;  // last interior plane
-    const double cxf = certx ? 1.0 : 0.0;
     // ZB: a step at the ends of the march or next to a z face (range and
     // face tests per plane); the steady steps between take every stage in
     // range and no z face, so those tests fold away, and in an interior tile
@@ -354,9 +357,10 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         constexpr bool E = decltype(Ec)::value;
         constexpr int P = decltype(Pc)::value;
         constexpr bool ZB = decltype(Zc)::value;
+        // a: a signed residual (APX) or its magnitude (res1); |a| enters the max
         auto rmax = [&](double& m, bool ok, bool ow, double a) __attribute__((always_inline)) {
-            if constexpr (!ZB && !BND) m = rb2_vmax(m, a);
-            else m = umax(ok && ow, a, m);
+            if constexpr (!ZB && !BND) m = rb2_vmax_abs(m, a);
+            else m = umax(ok && ow, fabs(a), m);
         };
         auto certv = [&](bool ok, bool ow, double v) __attribute__((always_inline)) {
             if constexpr (!ZB) {
@@ -415,10 +419,10 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         const double sx1 = xrp + Xc.x, sy1 = xhi.y + xlo.y, sz1 = Xp.y + Xm.y;
         double r1v, t1;
         if (e == 0) {
-            const double v = rb2_sorc<APX>(rc, cf.slow, Xc.x, sx0, sy0, sz0, b1.x, &t1);
+            const double v = rb2_sorc<APX>(cf, Xc.x, sx0, sy0, sz0, b1.x, &t1);
             r1v = (pin1 && in0) ? v : Xc.x;
         } else {
-            const double v = rb2_sorc<APX>(rc, cf.slow, Xc.y, sx1, sy1, sz1, b1.y, &t1);
+            const double v = rb2_sorc<APX>(cf, Xc.y, sx1, sy1, sz1, b1.y, &t1);
             r1v = (pin1 && in1) ? v : Xc.y;
         }
         {
@@ -434,15 +438,6 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             }
             rmax(mX, oka, own0, a0);
             rmax(mX, oka, own1, a1);
-            if constexpr (APX) {
-                if constexpr (!ZB) {
-                    // X's values when certx (an inf times 0 is a NaN, dropped)
-                    M = rb2_vmax(M, rb2_max_abs2(Xc.x, Xc.y) * cxf);
-                } else {
-                    cert(oka && certx && own0, Xc.x);
-                    cert(oka && certx && own1, Xc.y);
-                }
-            }
             certv(oka, owe, r1v);
             pin();
         }
@@ -464,7 +459,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         double y1v;
         {
             const double sx = (e == 0) ? r1c + r1sd : r1sd + r1c;
-            const double v = rb2_sorc<APX>(rc, cf.slow, comp(Xm, e), sx, r1up + r1dn, r1v + r1m,
+            const double v = rb2_sorc<APX>(cf, comp(Xm, e), sx, r1up + r1dn, r1v + r1m,
                                           comp(br[B0], e));
             y1v = (pin0 && ine) ? v : comp(Xm, e);
             certv(ok0, owe, y1v);
@@ -490,7 +485,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
             const double sx = rt + lf, sy = yup + ydn, sz = zp + zm;
             const double2 bm = br[Bm1];
             double t3;
-            const double v = rb2_sorc<APX>(rc, cf.slow, cen, sx, sy, sz, comp(bm, e), &t3);
+            const double v = rb2_sorc<APX>(cf, cen, sx, sy, sz, comp(bm, e), &t3);
             r2v = (pinm && ine) ? v : cen;
             // the residual of Y1' at plane q-1: cell e (first colour) shares the
             // update's sums; cell 1-e (second colour, value ob) reads the
@@ -538,7 +533,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
                 lf = f1l ? cen : ow;
                 rt = f1r ? cen : wsd;
             }
-            const double v = rb2_sorc<APX>(rc, cf.slow, cen, rt + lf, wup + wdn, zp + zm, bq2);
+            const double v = rb2_sorc<APX>(cf, cen, rt + lf, wup + wdn, zp + zm, bq2);
             const double y2v = (pind && ine) ? v : cen;
             certv(okd, owe, y2v);
             pin();
@@ -646,9 +641,9 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
                        jlo + RB2_TR - 1 <= g.ny - 3);
     double mX = 0.0, mY = 0.0, M = 0.0;
     if (bnd)
-        rb2_march<APX, FL, true>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M);
+        rb2_march<APX, FL, true>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, mX, mY, M);
     else
-        rb2_march<APX, FL, false>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, certx, mX, mY, M);
+        rb2_march<APX, FL, false>(L, g, cf, X, Y, rhs, c, r, i0, j, kb, ke, mX, mY, M);
     // ---- the sweep's maxima: partials[4 b + 0..2]; the last workgroup decides ----
     mX = wave_max(mX);
     mY = wave_max(mY);
@@ -709,6 +704,8 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
         }
         __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (APX) {
+            // X's own values (k_rb2_xmax; a NaN there fails the test too)
+            if (certx && !(st->xmax <= tM)) tM = st->xmax;
             if (!(tM <= cf.mlim)) {
                 st->done = 1;
                 st->status = ST_RB2_UNCERT;
@@ -743,6 +740,36 @@ static __global__ __launch_bounds__(256) void k_rb2_bmax(Geo g, const double* __
     if ((threadIdx.x & 63) == 0 && m > 0.0)
         __hip_atomic_fetch_max((gu64*)&st->bmax, (unsigned long long)__double_as_longlong(m),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// max |X| over the interior into st->xmax (zeroed by the host first): the
+// certification of X's own values for a sweep whose input did not come
+// from a k_rb2 sweep (certx); a NaN's bits order above every finite value,
+// so a NaN fails the sweep's range test as before
+static __global__ __launch_bounds__(256) void k_rb2_xmax(Geo g, const double* __restrict__ X,
+                                                         RxState* st) {
+    double m = 0.0;
+    const int ni = g.nx - 2, nj = g.ny - 2;
+    const long long plane = (long long)ni * nj;
+    const long long total = plane * (g.nz - 2);
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int k = 1 + (int)(e / plane);
+        const long long q = e % plane;
+        const int jj = 1 + (int)(q / ni), ii = 1 + (int)(q % ni);
+        const double v = fabs(X[(long long)k * g.ps + (long long)jj * g.px + ii]);
+        m = (v > m || v != v) ? v : m;
+    }
+    // the bit patterns of non-negative values (and NaN above them) order as
+    // unsigned integers
+    unsigned long long b = (unsigned long long)__double_as_longlong(m);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_down(b, off, 64);
+        b = o > b ? o : b;
+    }
+    if ((threadIdx.x & 63) == 0 && b != 0)
+        __hip_atomic_fetch_max((gu64*)&st->xmax, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // resume the loop after the host resolved a stop: clear the decision, and
