@@ -137,6 +137,7 @@ struct hip_proj_ctx {
     CgState* st = nullptr;
     RxState* rxst = nullptr;             // fused relaxation loop state
     RxState* rxst2 = nullptr;            // scratch state of k_rb2's recompute sweeps
+    void* rb2dec = nullptr;              // k_rb2's decision constants (Rb2Dec, rb2.hpp)
     SGeo r2geo{};                        // two-iterations-per-sweep RB-SOR tiling (k_rb2)
     SGeo ccgeo{};                        // fused single-reduction CG tiling (k_ccf)
     SGeo cc_edge{}, cc_int{};            // slabs: k_ccf on the edge planes, then the rest

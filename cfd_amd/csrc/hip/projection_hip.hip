@@ -615,20 +615,21 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
     ST_TRY(ensure_aux(c, true, true));
     if (!c->rxst) HIP_TRY(hipMalloc((void**)&c->rxst, sizeof(RxState)));
     if (!c->rxst2) HIP_TRY(hipMalloc((void**)&c->rxst2, sizeof(RxState)));
+    if (!c->rb2dec) HIP_TRY(hipMalloc((void**)&c->rb2dec, sizeof(Rb2Dec)));
     Rb2Coef cf;
     cf.rc = rc;
     cf.k2 = 2.0 * (rc.rdx2 + rc.rdy2 + rc.inv_dz2);
-    cf.kb = rc.rdx2 + rc.rdy2 + rc.inv_dz2;
-    cf.escale = 1.0;
-    cf.mlim = 0x1p800;
     cf.slow = 0x1p-900;
     cf.nif = -rc.inv_factor;
+    double escale = 1.0, mlim = 0x1p800;
     if (c->env.rb2_test) {  // tests: force the host paths
         const int v = c->env.rb2_test;
-        if (v == 1) cf.escale = 1e300;  // every approximate decision ambiguous
-        if (v == 2) cf.mlim = 0.0;      // every sweep uncertified
-        if (v == 3) cf.slow = 1e300;    // every SOR update in the reference's arithmetic
+        if (v == 1) escale = 1e300;  // every approximate decision ambiguous
+        if (v == 2) mlim = 0.0;      // every sweep uncertified
+        if (v == 3) cf.slow = 1e300; // every SOR update in the reference's arithmetic
     }
+    hipExtLaunchKernelGGL(k_rb2_dec_init, dim3(1), dim3(64), 0, c->stream, c->ta, c->tb, 0,
+                          (Rb2Dec*)c->rb2dec, rc.rdx2 + rc.rdy2 + rc.inv_dz2, escale, mlim);
     // the fast division's range argument (rb2.hpp rb2_sorc) needs 1 <= 1/d^2 <= 2^60
     if (!(rc.rdx2 >= 1.0 && rc.rdy2 >= 1.0 && rc.rdx2 <= 0x1p60 && rc.rdy2 <= 0x1p60))
         apx = false;
@@ -676,12 +677,14 @@ static cfd_status_t relax_solve_rb2(hip_proj_ctx* c, const RelaxCoef& rc, double
                     hipExtLaunchKernelGGL((k_rb2<true, FLR>), dim3(nb2), dim3(1024), 0, c->stream,
                                           c->ta, c->tb, 0, g2, cf, (const double*)bx, by,
                                           (const double*)c->rhs, c->rxst, c->partials,
-                                          c->counter, cur, certx, xmap);
+                                          c->counter, cur, certx, xmap,
+                                          (const Rb2Dec*)c->rb2dec);
                 else
                     hipExtLaunchKernelGGL((k_rb2<false, FLR>), dim3(nb2), dim3(1024), 0,
                                           c->stream, c->ta, c->tb, 0, g2, cf, (const double*)bx,
                                           by, (const double*)c->rhs, c->rxst, c->partials,
-                                          c->counter, cur, certx, xmap);
+                                          c->counter, cur, certx, xmap,
+                                          (const Rb2Dec*)c->rb2dec);
             }, cur);
             log.push_back({cur, 2, bx, by});
             cur += 2;
@@ -1188,6 +1191,7 @@ static void free_ctx(hip_proj_ctx* c) {
     if (c->st) hipFree(c->st);
     if (c->rxst) hipFree(c->rxst);
     if (c->rxst2) hipFree(c->rxst2);
+    if (c->rb2dec) hipFree(c->rb2dec);
     if (c->partials) hipFree(c->partials);
     if (c->counter) hipFree(c->counter);
     if (c->red) hipFree(c->red);

@@ -78,15 +78,24 @@ constexpr int ST_RB2_UNCERT = 11;  // a value outside the certified range (host 
 struct Rb2Coef {
     RelaxCoef rc;
     double k2;   // 2 (RN(1/dx2) + RN(1/dy2) + inv_dz2): the centre weight of the approximation
-    double kb;   // 1/dx2 + 1/dy2 + inv_dz2 (error bound)
-    // test knobs (CFD_HIP_RB2_TEST): escale multiplies the residual bound
-    // (1e300: every decision ambiguous); mlim is the largest certified
-    // |value| (2^800; 0: every sweep uncertified); slow: a wave recomputes an
-    // SOR update in the reference's arithmetic when the smaller |neighbour
-    // sum| of one of its lanes is below it (2^-900; 1e300: every update)
-    double escale, mlim;
+    // slow: a wave recomputes an SOR update in the reference's arithmetic
+    // when the smaller |neighbour sum| of one of its lanes is below it
+    // (2^-900; test knob CFD_HIP_RB2_TEST=3: 1e300, every update)
     double slow;
     double nif;  // -inv_factor: pn = t * nif is RN(-t * inv_factor) bit for bit (RN is odd)
+};
+
+// The sweep's decision constants, read by the last workgroup only. They sit
+// in device memory (k_rb2_dec_init, once per solve) rather than in the
+// kernel's arguments: an argument stays in a scalar register across the
+// whole march, and the march's scalar registers are full (the compiler then
+// spills loop operands and reloads them with v_readlane every step).
+struct Rb2Dec {
+    double kb;      // 1/dx2 + 1/dy2 + inv_dz2 (error bound)
+    // test knobs (CFD_HIP_RB2_TEST): escale multiplies the residual bound
+    // (1e300: every decision ambiguous); mlim is the largest certified
+    // |value| (2^800; 0: every sweep uncertified)
+    double escale, mlim;
 };
 
 // LDS of one k_rb2 workgroup (148 KB): X by plane parity, and the one-colour
@@ -614,7 +623,7 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
                                                        const double* __restrict__ rhs,
                                                        RxState* st, double* partials,
                                                        unsigned* counter, int s, int certx,
-                                                       int xmap) {
+                                                       int xmap, const Rb2Dec* __restrict__ dec) {
     __shared__ Rb2Lds L;
     if (st->done) return;
     // tile order: xmap = 1 gives each XCD a contiguous range of tiles
@@ -706,13 +715,13 @@ static __global__ __launch_bounds__(1024, 4) void k_rb2(SGeo g, Rb2Coef cf,
         if constexpr (APX) {
             // X's own values (k_rb2_xmax; a NaN there fails the test too)
             if (certx && !(st->xmax <= tM)) tM = st->xmax;
-            if (!(tM <= cf.mlim)) {
+            if (!(tM <= dec->mlim)) {
                 st->done = 1;
                 st->status = ST_RB2_UNCERT;
                 st->res_it = s;
                 return;
             }
-            const double E = 32.0 * 0x1p-53 * (4.0 * tM * cf.kb + st->bmax) * cf.escale;
+            const double E = 32.0 * 0x1p-53 * (4.0 * tM * dec->kb + st->bmax) * dec->escale;
             if (rb2_decide(st, tX, E, s) && !st->done) rb2_decide(st, tY, E, s + 1);
         } else {
             rx_finish(st, tX, s);
@@ -770,6 +779,14 @@ static __global__ __launch_bounds__(256) void k_rb2_xmax(Geo g, const double* __
     }
     if ((threadIdx.x & 63) == 0 && b != 0)
         __hip_atomic_fetch_max((gu64*)&st->xmax, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+static __global__ void k_rb2_dec_init(Rb2Dec* d, double kb, double escale, double mlim) {
+    if (threadIdx.x == 0) {
+        d->kb = kb;
+        d->escale = escale;
+        d->mlim = mlim;
+    }
 }
 
 // resume the loop after the host resolved a stop: clear the decision, and
