@@ -701,11 +701,13 @@ def run_convection(args, rank, world, local, comm, lib, torch, dist):
                     "traffic_source": traffic_src,
                     "algorithmic_bytes": BYTES_RB2_SWEEP * n_loc,
                     "bytes_per_cell": BYTES_RB2_SWEEP, "iterations_per_sweep": 2,
-                    # what bounds it: fp64 VALU issue and the per-step barrier,
-                    # not HBM (r04 PMC at 1024^2 x 512: VALU busy ~0.5 of the
-                    # step, the XCD-contiguous tile map fetches 22 % fewer bytes
-                    # in the same time; profiles/r04_rb2_pmc_xmap*.jsonl)
-                    "limiter": "fp64 VALU issue + per-plane barrier (DESIGN.md §3 r04)",
+                    # what bounds it (r06, after the VALU trim): the bytes it
+                    # moves, 31.7 fetched + 8.1 written B/cell per sweep at the
+                    # box's copy rate, half the reads the tile's halo; the
+                    # on-chip part alone runs 1.17 ms per iteration
+                    # (profiles/r06ah_rb2_xmap_kc.jsonl, the diagnostic build)
+                    "limiter": ("HBM bytes of the tile halo (no-memory build 1.17 vs 1.66 ms per "
+                                "iteration, DESIGN.md §3 r06)"),
                     "avg_sweep_ms": round(avg, 4), "sweeps": sweeps, "launches": r2n,
                     "one_iteration_sweeps": rn}
         else:
