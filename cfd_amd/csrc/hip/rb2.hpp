@@ -308,9 +308,17 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         if constexpr (RB2_DIAG) return ld2(X, colx);
         return ld2(X + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
     };
-    auto ldr = [&](int k) -> double2 {
-        if constexpr (RB2_DIAG) return ld2(rhs, colx);
-        return ld2(rhs + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
+    // rhs enters S1 first, whose values are valid one row inside the loaded
+    // tile: the tile's outer rows (0, TR - 1) never load it and keep the
+    // ring's zeros (the halo lanes' values stay ordinary); 2 of the 32 rows'
+    // rhs lines. A masked load into the ring slot, no select.
+    const bool rrow = r >= 1 && r <= RB2_TR - 2;
+    auto ldr = [&](double2& dst, int k) __attribute__((always_inline)) {
+        if constexpr (RB2_DIAG) {
+            dst = ld2(rhs, colx);
+        } else {
+            if (rrow) dst = ld2(rhs + (long long)min(max(k, 0), g.nz - 1) * g.ps, colx);
+        }
     };
     auto comp = [](const double2& v, int e) __attribute__((always_inline)) {
         return e == 0 ? v.x : v.y;
@@ -321,8 +329,8 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
     xr[1] = ldx(q0 + 1);
     xr[2] = ldx(q0 + 2);
     xr[3] = make_double2(0.0, 0.0);
-    br[0] = br[1] = br[3] = make_double2(0.0, 0.0);
-    br[2] = ldr(q0 + 1);
+    br[0] = br[1] = br[2] = br[3] = make_double2(0.0, 0.0);
+    ldr(br[2], q0 + 1);
     // X_{q0+1} into the X slot step q0 reads: LDS slots count planes from q0
     st(RB2_PX + 2, xr[1].x);
     st(RB2_PX + 3, xr[1].y);
@@ -393,7 +401,7 @@ __device__ __forceinline__ void rb2_march(Rb2Lds& L, const SGeo& g, const Rb2Coe
         // rhs_{q-2} leaves its slot to rhs_{q+2}
         const double bq2 = comp(br[B2], e);
         xr[X3] = ldx(q + 3);
-        br[B2] = ldr(q + 2);
+        ldr(br[B2], q + 2);
         __syncthreads();
         const int qa = q + 1, qc = q - 1, qd = q - 2;
         const bool pin1 = !ZB || (qa >= 1 && qa <= nzi), pin0 = !ZB || (q >= 1 && q <= nzi);
