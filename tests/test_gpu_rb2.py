@@ -114,3 +114,35 @@ def test_rb2_tiny_front_bitwise(hip_lib, monkeypatch, mode, iters):
     assert sth.initial_residual == sto.initial_residual
     assert sth.final_residual == sto.final_residual
     np.testing.assert_array_equal(xh, xo)
+
+
+@pytest.mark.parametrize("iters", [5, 6])
+def test_rb2_uncertified_input_bitwise(hip_lib, monkeypatch, capfd, iters):
+    """An initial guess with one interior value above the certified range
+    (|v| > 2^800): the first two-iteration sweep certifies its input X by the
+    k_rb2_xmax pre-pass (r06; the march no longer certifies X itself), fails,
+    and the host reruns with one iteration per sweep (k_rb1); bitwise against
+    the oracle, and the launch log shows the uncertified stop."""
+    monkeypatch.setenv("CFD_HIP_RB2", "1")
+    monkeypatch.setenv("CFD_HIP_RB2_LOG", "1")
+    nx, ny, nz = 70, 66, 40
+    rng = np.random.default_rng(11)
+    rhs = rng.standard_normal((nz, ny, nx))
+    x0 = 0.1 * rng.standard_normal((nz, ny, nx))
+    x0[20, 30, 35] = 1e245  # 2^800 ~ 6.7e240
+    d = 1.0 / (nx - 1)
+    prm = oracle.poisson_params(max_iterations=iters, tolerance=0.0, absolute_tolerance=0.0)
+    xo = x0.copy()
+    so, sto = oracle.redblack_solve(xo, rhs, d, d, d, prm)
+    assert np.isfinite(xo).all()
+    ctx = api.HipProjection(nx, ny, nz)
+    xh = x0.copy()
+    sh, sth = ctx.poisson_solve(A.HIP_POISSON_REDBLACK, xh, rhs, d, d, d, prm)
+    ctx.close()
+    assert sh == so
+    assert (sth.iterations, sth.status) == (sto.iterations, sto.status)
+    assert sth.initial_residual == sto.initial_residual
+    assert sth.final_residual == sto.final_residual
+    np.testing.assert_array_equal(xh, xo)
+    err = capfd.readouterr().err
+    assert "1 uncertified" in err, err[-2000:]
