@@ -538,7 +538,7 @@ def main():
                               "sum d memtime / sum d memrealtime (rank 0)")},
             "box": box_id(torch, local),
             "placement": {"probe_ms_per_iter": place_ms, "picked": place_pick,
-                          "how": ("the CG fields allocated 4 times at context creation, 24 "
+                          "how": ("the CG fields allocated 6 times at context creation, 40 "
                                   "assignments of those buffers to the 7 roles each timed on "
                                   "a 16-iteration probe solve, the fastest kept "
                                   "(projection_hip.hip placement_draws)")},

@@ -1831,17 +1831,20 @@ static hip_proj_ctx* create_common(size_t nx, size_t ny, size_t nz_local, size_t
     // placement draws of the single-reduction CG's fields (3-D contexts of
     // >= 2^24 cells, one device or one Z-slab rank; see placement_draws)
     {
-        // a pool of 4 allocated sets and 24 probes: the 4 sets as allocated,
-        // then 20 random assignments of pool buffers to the seven roles.
+        // a pool of 6 allocated sets and 40 probes: the 6 sets as allocated,
+        // then 34 random assignments of pool buffers to the seven roles.
         // r06x, 512^3, contexts of one process (ms per iteration): none
         // 1.109-1.201; 8 sets 1.037-1.126; 2 sets + 16 probes 1.033-1.047
         // with one 1.198 (a pool with no good pair); 4 sets + 16 probes
-        // 1.030-1.044 (profiles/r06x_placement_strategies.jsonl).
+        // 1.030-1.044 (profiles/r06x_placement_strategies.jsonl). r06ar,
+        // twelve contexts each: 4 sets + 24 probes 1.034-1.048 (mean
+        // 1.0400), 6 + 40 1.032-1.042 (1.0372), 4 + 48 1.036-1.061
+        // (profiles/r06ar_placement_draws.jsonl); ~0.3 s more per context.
         // CFD_HIP_PLACEMENT_DRAWS = sets (1: off), _TRIALS = probes
         const char* e = getenv("CFD_HIP_PLACEMENT_DRAWS");
-        const int draws = e ? atoi(e) : 4;
+        const int draws = e ? atoi(e) : 6;
         const char* et = getenv("CFD_HIP_PLACEMENT_TRIALS");
-        const int trials = et ? std::max(1, atoi(et)) : 24;
+        const int trials = et ? std::max(1, atoi(et)) : 40;
         const long long cells = (long long)nx * (long long)ny * (long long)nz_local;
         if (c->cfg.cg_variant == 1 && nz_local >= 3 && cells >= (1LL << 24) && draws > 1 &&
             c->ccgeo.tiles_x > 0 && !c->env.ccf_off) {

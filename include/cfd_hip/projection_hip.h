@@ -245,9 +245,9 @@ CFD_HIP_EXPORT void hip_proj_get_timing(hip_proj_ctx_t* ctx, double* total_ms, l
 CFD_HIP_EXPORT cfd_status_t hip_proj_get_clock_sample(hip_proj_ctx_t* ctx, double* mhz,
                                                       long long* workgroups);
 /* Placement draws of a large single-reduction context (3-D, >= 2^24 cells; a
- * Z-slab rank probes its own fields as one device, nothing collective): at creation its seven CG fields are allocated 4 times
- * (CFD_HIP_PLACEMENT_DRAWS) and 24 assignments of those buffers to the seven
- * roles (CFD_HIP_PLACEMENT_TRIALS: the 4 sets, then random ones) are timed on a
+ * Z-slab rank probes its own fields as one device, nothing collective): at creation its seven CG fields are allocated 6 times
+ * (CFD_HIP_PLACEMENT_DRAWS) and 40 assignments of those buffers to the seven
+ * roles (CFD_HIP_PLACEMENT_TRIALS: the 6 sets, then random ones) are timed on a
  * short probe solve; the fastest is kept. Writes each draw's probe time (ms per CG iteration) into
  * ms_per_iter[0 .. min(capacity, count) - 1] and the kept draw's index into
  * *picked (-1: no draws); returns the number of draws. */

@@ -209,3 +209,36 @@ def test_field_stagger_is_bitwise_neutral(hip_lib, monkeypatch):
         for k in ("u", "v", "w", "p"):
             a, b = out[("0", cgv)][k], out[(None, cgv)][k]
             assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (cgv, k)
+
+
+def test_placement_draws_are_bitwise_neutral(hip_lib, monkeypatch):
+    """The placement draws (r06; a single-reduction context of >= 2^24 cells
+    allocates its CG fields six times and times 40 assignments of them to the
+    seven roles) choose where the fields sit, never what is computed: the
+    probe records 40 positive times and keeps the fastest, and cavity steps
+    are bitwise those of a context without draws (CFD_HIP_PLACEMENT_DRAWS=1)."""
+    n, nz = 256, 257  # 16.84 M cells, just above 2^24
+    out, place = {}, {}
+    for draws in ("1", None):
+        if draws is None:
+            monkeypatch.delenv("CFD_HIP_PLACEMENT_DRAWS", raising=False)
+        else:
+            monkeypatch.setenv("CFD_HIP_PLACEMENT_DRAWS", draws)
+        g, f, p = cases.cavity(n, n, nz, Re=400.0, dt=2e-4)
+        ctx = api.HipProjection(n, n, nz, cg_variant=1)
+        try:
+            place[draws] = ctx.placement()
+            api.cavity_bc(f, 1.0)
+            ctx.upload(f)
+            for _ in range(2):
+                assert ctx.step_device(g, p) == A.CFD_SUCCESS, api._native.last_error()
+            out[draws] = {k: ctx.get_field(fid).copy() for k, fid in
+                          (("u", A.HIP_FIELD_U), ("p", A.HIP_FIELD_P))}
+        finally:
+            ctx.close()
+    assert place["1"] == ([], -1)
+    ms, pick = place[None]
+    assert len(ms) == 40 and all(v > 0 for v in ms)
+    assert 0 <= pick < 40 and ms[pick] == min(ms)  # (times rounded to 0.1 us)
+    for k in ("u", "p"):
+        assert np.array_equal(out["1"][k].view(np.uint64), out[None][k].view(np.uint64)), k
